@@ -1,0 +1,220 @@
+#!/usr/bin/env python3
+"""bench.py -- device-resident encode+decode goodput of the MI355X RS engine.
+
+Metric (BASELINE.json): "encode+decode goodput GiB/s (device-resident) at
+symbols x symbol_size; %HBM roofline".  Workload at N=1: BASELINE.json
+configs[2] -- symbols=64, symbol_size=1000000, loss_rate=0.5 (32 erased /
+32 parity symbols), 1024 blocks batched on one MI355X.
+
+One step = the timed regions of benchmark/isa_throughput over the whole batch:
+  encode_all  -- parity of every block (isa.cpp:69-79), and
+  decode_all  -- decode matrix + inversion + reconstruction of the erased
+                 originals of every block (isa.cpp:169-213),
+with sources, parity and outputs resident in HBM when the timed region starts.
+Goodput = (parity bytes + recovered bytes) / time, as the reference's
+measurement() counts output bytes (throughput_benchmark.hpp:37-67).
+
+Multi-GPU: one process per GPU (torch.distributed, RCCL backend only for the
+barrier and the max-over-ranks timing); each rank owns its own 1024 blocks
+(weak scaling, no collective on the data path).
+
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "storage-benchmarks_amd"))
+
+CONFIGS = {
+    # name: (symbols, symbol_size, loss_rate, blocks per GPU)
+    "c2": (16, 1000000, 0.25, 1),
+    "c3": (64, 1000000, 0.5, 1024),
+    "c4": (64, 32000, 0.5, 32768),      # 1M blocks streamed: 32768 resident per pass
+    "c5": (100, 1000000, 0.2, 512),     # 4096 blocks over 8 GPUs = 512 per GPU
+}
+HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md chip table, spec
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=10)
+    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    p.add_argument("--blocks", type=int, default=None, help="blocks per GPU (override)")
+    p.add_argument("--seed", type=int, default=1)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-threads", type=int, default=None)
+    p.add_argument("--no-verify", action="store_true")
+    p.add_argument("--traffic", default=None,
+                   help="JSON with PMC-derived HBM bytes per launch (profiles/)")
+    return p.parse_args()
+
+
+def dist_env():
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    return rank, world, local
+
+
+def cpu_baseline(k, e, L, threads):
+    """ISA-L base C compiled from the reference (oracle/_ref, kind "reference")
+    or our restatement timed the same way (kind "port"), on a bounded sample:
+    `threads` workers x 1 block of the same geometry, encode + decode timed
+    exactly as isa.cpp's timed regions."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_lib
+    if not oracle_lib.have_reference():
+        return None
+    ref = oracle_lib.Reference()
+    r = ref.cpu_bench(k, e, L, threads, 1, 7)
+    out_bytes = 2.0 * e * L * threads
+    t = r["max_thread_s"]
+    return {"value": out_bytes / t / 2 ** 30, "unit": "GiB/s", "cores": threads,
+            "kind": "reference",
+            "sample": f"{threads} threads x 1 block (k={k}, e={e}, L={L}) encode+decode, "
+                      f"ISA-L 2.13 ec_base.c scalar path (no yasm for the AVX2 asm), "
+                      f"{t:.1f} s per thread, failures={r['failures']}",
+            "encode_s": r["enc_s"] / threads, "decode_s": r["dec_s"] / threads}
+
+
+def main():
+    args = parse()
+    rank, world, local = dist_env()
+    import torch
+    import torch.distributed as dist
+
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", init_method="env://")
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+
+    import rsgpu
+
+    k, L, loss, B = CONFIGS[args.config]
+    if args.blocks:
+        B = args.blocks
+    e = int(math.ceil(k * loss))
+    ctx = rsgpu.Context(dev.index)
+    ctx.set_torch_stream()
+
+    # rank r owns global blocks [r*B, (r+1)*B): independent shard, no exchange
+    enc = rsgpu.GpuEncoder(k, L, e, blocks=B, seed=args.seed, ctx=ctx, block0=rank * B)
+    dec = rsgpu.GpuDecoder(k, L, e, blocks=B, seed=args.seed, ctx=ctx, block0=rank * B)
+    torch.cuda.synchronize()
+
+    # HIP events on the stream the kernels are launched on (torch's current
+    # stream, handed to the engine by set_torch_stream)
+    st = torch.cuda.current_stream()
+    names = ("enc", "prep", "apply")
+    evs = [{n: (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            for n in names} for _ in range(args.steps)]
+
+    def step(ev=None):
+        if ev:
+            ev["enc"][0].record(st)
+        enc.encode_all()
+        if ev:
+            ev["enc"][1].record(st)
+            ev["prep"][0].record(st)
+        dec.ctx.decode_prepare(k, e, L, enc.pitch, B, enc.src, enc.par, dec.err, dec.out,
+                               dec.ws, dec.status)
+        if ev:
+            ev["prep"][1].record(st)
+            ev["apply"][0].record(st)
+        dec.ctx.decode_apply(k, e, L, enc.pitch, B, enc.src, enc.par, dec.out, dec.ws,
+                             dec.status)
+        dec._decoded = True
+        if ev:
+            ev["apply"][1].record(st)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if not args.no_verify and args.warmup > 0:
+        assert dec.is_complete(), "decode matrix singular"
+        assert dec.verify_data(enc), "recovered symbols differ from the originals"
+    torch.cuda.synchronize()
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(evs[i])
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    acc = {n: sum(ev[n][0].elapsed_time(ev[n][1]) for ev in evs) for n in names}
+    if world > 1:
+        dist.barrier()
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+
+    ok = True
+    if not args.no_verify:
+        ok = dec.is_complete() and dec.verify_data(enc)
+
+    out_bytes_step = 2.0 * e * L * B            # parity + recovered, per rank
+    total_out = out_bytes_step * args.steps * world
+    value = total_out / elapsed / 2 ** 30
+    ms_step = elapsed / args.steps * 1e3
+    alg_bytes = float((k + e) * L * B)          # per launch: read k rows, write e rows
+    avg = {n: acc[n] / args.steps for n in acc}  # ms
+    dom = "apply" if avg["apply"] >= avg["enc"] else "enc"
+    dom_name = {"apply": "k_dot_generic (decode apply)", "enc": "k_rs_encode_lh (encode)"}[dom]
+    achieved = alg_bytes / (avg[dom] * 1e-3) / 1e9
+    traffic = None
+    if args.traffic and os.path.exists(args.traffic):
+        traffic = json.load(open(args.traffic)).get(dom)
+    step_frac = (2 * alg_bytes) / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBPS
+
+    line = {
+        "metric": "encode+decode goodput GiB/s (device-resident) at symbols x symbol_size; "
+                  "%HBM roofline",
+        "value": round(value, 2), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+        "config": {"workload": f"isa_throughput {args.config}: symbols={k} symbol_size={L} "
+                               f"loss_rate={loss} erased={e} blocks_per_gpu={B}",
+                   "symbols": k, "symbol_size": L, "loss_rate": loss, "erased": e,
+                   "blocks_per_gpu": B, "parallelism": f"blocks sharded x{world}, no collective"},
+        "hbm_roofline_frac_step": round(step_frac, 4),
+        "encode_ms": round(avg["enc"], 3), "decode_prepare_ms": round(avg["prep"], 3),
+        "decode_apply_ms": round(avg["apply"], 3),
+        "encode_GBps_alg": round(alg_bytes / (avg["enc"] * 1e-3) / 1e9, 1),
+        "decode_apply_GBps_alg": round(alg_bytes / (avg["apply"] * 1e-3) / 1e9, 1),
+        "verified": ok,
+        "roofline": {"bound": "hbm", "kernel": dom_name, "achieved": round(achieved, 1),
+                     "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
+                     "alg_bytes_per_launch": alg_bytes},
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+        try:
+            line["cpu_baseline"] = cpu_baseline(k, e, L, threads)
+        except Exception as ex:  # reported, never fatal for the GPU number
+            line["cpu_baseline"] = {"error": str(ex)}
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    if not ok:
+        sys.exit(1)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,162 @@
+/*
+ * rsgpu.h -- C ABI of the MI355X-native Reed-Solomon GF(2^8) erasure engine
+ * (librsgpu.so).  Drop-in boundary for the hot path of
+ * steinwurf/storage-benchmarks' benchmark/isa_throughput: the plugin calls
+ * the ISA-L 2.13 C ABI (isa-l_open_src_2.13/isa/erasure_code.h) from
+ * isa_encoder::encode_all (benchmark/isa_throughput/isa.cpp:69-79) and
+ * isa_decoder::decode_all (isa.cpp:169-213).  Every entry point below names
+ * the reference interface it replaces.
+ *
+ * Conventions (same as the ISA-L ABI):
+ *   - plain pointers and sizes, C linkage, no exceptions, no allocation of
+ *     caller data: the caller owns every buffer (host or device);
+ *   - status returns: RSGPU_OK (0) or a negative RSGPU_ERR_* code; the
+ *     context keeps a message for rsgpu_last_error();
+ *   - work is enqueued on the context's HIP stream (hipStream_t passed as
+ *     void*); nothing synchronises unless the function says so;
+ *   - one context per device and host thread; distinct contexts are
+ *     independent (one process or thread per GPU).
+ *
+ * Device data layout of the batched calls ("blocks"): row r of block b of a
+ * buffer with R rows per block lives at base + (b*R + r)*pitch, pitch >= len.
+ * Source rows are the k original symbols, parity rows the e = m-k coded
+ * symbols (gf_gen_rs_matrix rows k..m-1), exactly as isa_encoder's m_buffs
+ * (isa.cpp:46-58) but contiguous in HBM.
+ */
+#ifndef RSGPU_H
+#define RSGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RSGPU_OK 0
+#define RSGPU_ERR_ARG (-1)
+#define RSGPU_ERR_HIP (-2)
+#define RSGPU_ERR_SINGULAR (-3)
+#define RSGPU_ERR_NOMEM (-4)
+#define RSGPU_ERR_UNSUPPORTED (-5)
+
+#define RSGPU_MAX_SOURCES 250 /* TEST_SOURCES, isa.cpp:25-27 */
+
+typedef struct rsgpu_ctx rsgpu_ctx;
+
+/* ---- version / context -------------------------------------------------- */
+
+/* "major.minor.patch" of the engine */
+const char *rsgpu_version(void);
+
+/* Binds the calling thread to HIP device `device` and creates a context whose
+ * stream is the device's null stream until rsgpu_set_stream(). */
+int rsgpu_create(int device, rsgpu_ctx **out);
+int rsgpu_destroy(rsgpu_ctx *ctx);
+int rsgpu_set_stream(rsgpu_ctx *ctx, void *hip_stream);
+void *rsgpu_get_stream(rsgpu_ctx *ctx);
+int rsgpu_synchronize(rsgpu_ctx *ctx);
+const char *rsgpu_last_error(rsgpu_ctx *ctx);
+
+/* Device memory helpers for C/C++ callers without another allocator. */
+int rsgpu_malloc(rsgpu_ctx *ctx, void **dptr, size_t bytes);
+int rsgpu_free(rsgpu_ctx *ctx, void *dptr);
+int rsgpu_memcpy_h2d(rsgpu_ctx *ctx, void *dst, const void *src, size_t bytes);
+int rsgpu_memcpy_d2h(rsgpu_ctx *ctx, void *dst, const void *src, size_t bytes);
+
+/* ---- host GF(2^8) helpers: the ISA-L C ABI, same arguments/semantics ----- */
+
+/* erasure_code.h gf_mul / gf_inv (isa/ec_base.c:36-60) */
+unsigned char rsgpu_gf_mul(unsigned char a, unsigned char b);
+unsigned char rsgpu_gf_inv(unsigned char a);
+/* erasure_code.h:898 gf_gen_rs_matrix (isa/ec_base.c:62-79) */
+void rsgpu_gf_gen_rs_matrix(unsigned char *a, int m, int k);
+/* erasure_code.h gf_gen_cauchy1_matrix (isa/ec_base.c:81-97) */
+void rsgpu_gf_gen_cauchy1_matrix(unsigned char *a, int m, int k);
+/* erasure_code.h:924 gf_invert_matrix (isa/ec_base.c:99-152): destroys `in`,
+ * returns 0 or -1 when singular. */
+int rsgpu_gf_invert_matrix(unsigned char *in, unsigned char *out, const int n);
+/* erasure_code.h gf_vect_mul_init (isa/ec_base.c:157-262): 32-byte table */
+void rsgpu_gf_vect_mul_init(unsigned char c, unsigned char *tbl);
+/* erasure_code.h:74 ec_init_tables (isa/ec_highlevel_func.c:33-43) */
+void rsgpu_ec_init_tables(int k, int rows, unsigned char *a, unsigned char *gftbls);
+
+/* ---- device, ISA-L-shaped ------------------------------------------------ */
+
+/* erasure_code.h:98 ec_encode_data (isa/ec_multibinary.asm:112-162 dispatch,
+ * isa/ec_highlevel_func.c:106-135 avx2 split): coding[r][i] =
+ * XOR_j c[r][j]*data[j][i].  `gftbls` is HOST memory in ISA-L's 32-byte table
+ * format (as produced by ec_init_tables); `data` / `coding` are HOST arrays
+ * of DEVICE pointers; any len >= 0 and any alignment. */
+int rsgpu_ec_encode_data(rsgpu_ctx *ctx, int len, int k, int rows, const unsigned char *gftbls,
+                         unsigned char **data, unsigned char **coding);
+
+/* erasure_code.h ec_encode_data_update (isa/ec_highlevel_func.c:139-252,
+ * isa/ec_base.c:307-321): coding[r][i] ^= c[r][vec_i] * data[i]. */
+int rsgpu_ec_encode_data_update(rsgpu_ctx *ctx, int len, int k, int rows, int vec_i,
+                                const unsigned char *gftbls, unsigned char *data,
+                                unsigned char **coding);
+
+/* ---- device, batched blocks (the benchmark hot path) --------------------- */
+
+/* isa_encoder::encode_all over `blocks` independent blocks (isa.cpp:69-79):
+ * parity[b][p] = XOR_j a[k+p][j] * src[b][j] with a = gf_gen_rs_matrix(k+e, k)
+ * when `coef` is NULL, else with the HOST e x k row-major matrix `coef`.
+ * src: [blocks][k] rows, parity: [blocks][e] rows, both at `pitch`. */
+int rsgpu_encode_blocks(rsgpu_ctx *ctx, int k, int e, size_t len, size_t pitch, size_t blocks,
+                        const unsigned char *d_src, unsigned char *d_parity,
+                        const unsigned char *coef);
+
+/* Device workspace needed by rsgpu_decode_blocks for this geometry. */
+size_t rsgpu_decode_workspace_bytes(int k, int e, size_t blocks);
+
+/* isa_decoder::decode_all over `blocks` blocks (isa.cpp:169-213): for block
+ * b the `e` erased ORIGINAL indices d_err[b][0..e-1] (ascending, as the
+ * std::set iterates, isa.cpp:150-153) are rebuilt from the surviving
+ * originals and all e parity rows.  On the device: survivor matrix ->
+ * gf_invert_matrix -> decode rows -> dot product into out[b][i] (symbol
+ * d_err[b][i]).  d_status[b] = 0, or -1 for a singular matrix ("BAD MATRIX",
+ * isa.cpp:185-190; that block's output is untouched).  d_workspace holds
+ * rsgpu_decode_workspace_bytes() bytes. */
+int rsgpu_decode_blocks(rsgpu_ctx *ctx, int k, int e, size_t len, size_t pitch, size_t blocks,
+                        const unsigned char *d_src, const unsigned char *d_parity,
+                        const unsigned char *d_err, unsigned char *d_out, void *d_workspace,
+                        int *d_status);
+
+/* The two halves of rsgpu_decode_blocks, for callers that time or reuse them:
+ * prepare = survivor matrix + gf_invert_matrix + decode tables + row pointers
+ * (isa.cpp:177-207) into d_workspace and d_status; apply = the dot product
+ * (isa.cpp:208-209) for blocks whose status is 0.  decode_blocks ==
+ * prepare followed by apply on the same stream. */
+int rsgpu_decode_prepare(rsgpu_ctx *ctx, int k, int e, size_t len, size_t pitch, size_t blocks,
+                         const unsigned char *d_src, const unsigned char *d_parity,
+                         const unsigned char *d_err, unsigned char *d_out, void *d_workspace,
+                         int *d_status);
+int rsgpu_decode_apply(rsgpu_ctx *ctx, int k, int e, size_t len, size_t pitch, size_t blocks,
+                       const unsigned char *d_src, const unsigned char *d_parity,
+                       unsigned char *d_out, void *d_workspace, const int *d_status);
+
+/* isa_decoder::verify_data (isa.cpp:215-229) on the device: adds to
+ * d_mismatch[b] the number of bytes where out[b][i] != src[b][d_err[b][i]]. */
+int rsgpu_verify_blocks(rsgpu_ctx *ctx, int k, int e, size_t len, size_t pitch, size_t blocks,
+                        const unsigned char *d_src, const unsigned char *d_out,
+                        const unsigned char *d_err, unsigned long long *d_mismatch);
+
+/* ---- synthetic workload (replaces rand(), isa.cpp:56-58, :137-146) ------- */
+
+/* Fills `rows` rows of `len` bytes at `pitch` with the seeded counter-based
+ * stream: bytes 8w..8w+7 of global row (row0 + r) = LE(mix(seed, row, w)). */
+int rsgpu_fill_synthetic(rsgpu_ctx *ctx, unsigned char *d_rows, size_t rows, size_t len,
+                         size_t pitch, uint64_t seed, uint64_t row0);
+
+/* Host: erasure lists of blocks blk0..blk0+blocks-1 into h_err[blocks][e]
+ * (e distinct originals per block, ascending), as the isa_decoder ctor draws
+ * them (isa.cpp:137-153) with a seeded generator. */
+int rsgpu_erasure_patterns(uint64_t seed, uint64_t blk0, size_t blocks, int k, int e,
+                           unsigned char *h_err);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RSGPU_H */

@@ -1,0 +1,52 @@
+// rs_kernels.h -- launch interface of the HIP kernels (internal to librsgpu).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace rsgpu {
+
+struct DotArgs {
+    const uint8_t* const* srcs;   // device [blocks][k] row pointers
+    uint8_t* const* dsts;         // device [blocks][rows] row pointers
+    const uint4* tabs4;           // device [blocks?][k][rows_pad] (perm tables, bits 0-5)
+    const uint32_t* ctab;         // device [blocks?][k][rows_pad] (perm table, bits 6-7)
+    long long tab_block_stride;   // coefficients between blocks' tables (0 = shared)
+    int k, rows, rows_pad;
+    long long len;                // bytes per row
+    long long blocks;
+    const int* status;            // optional [blocks]: skip blocks with status != 0
+    bool bytewise;                // pointers not 8-byte aligned: byte kernel
+};
+
+struct PrepArgs {
+    int k, e, rows_pad;
+    long long blocks;
+    const uint8_t* err;           // device [blocks][e]
+    const uint8_t* src; long long src_pitch;
+    const uint8_t* par; long long par_pitch;
+    uint8_t* out; long long out_pitch;
+    const uint8_t** surv_ptrs;    // device [blocks][k]
+    uint8_t** out_ptrs;           // device [blocks][e]
+    uint4* tabs4; uint32_t* ctab; long long tab_block_stride;
+    int* status;                  // device [blocks]
+};
+
+int generic_rows_per_pass(int rows);
+hipError_t launch_dot_generic(const DotArgs& a, hipStream_t st);
+bool rs_encode_specialized_available(int k, int e);
+hipError_t launch_rs_encode_specialized(int k, int e, const uint8_t* src, uint8_t* par,
+                                        long long pitch, long long len, long long blocks,
+                                        hipStream_t st);
+size_t decode_prepare_lds_bytes(int k);
+hipError_t launch_decode_prepare(const PrepArgs& a, hipStream_t st);
+hipError_t launch_fill_synth(uint8_t* dst, long long rows, long long len, long long pitch,
+                             unsigned long long seed, unsigned long long row0, hipStream_t st);
+hipError_t launch_compare_rows(const uint8_t* src, long long src_pitch, int k, const uint8_t* out,
+                               long long out_pitch, int e, const uint8_t* err, long long len,
+                               long long blocks, unsigned long long* mismatches, hipStream_t st);
+hipError_t launch_row_ptrs(const uint8_t* base, long long pitch, int rows_per_block,
+                           long long blocks, const uint8_t** out, hipStream_t st);
+hipError_t launch_update(const uint8_t* data, uint8_t* const* coding, const uint4* tabs4,
+                         const uint32_t* ctab, int rows, long long len, hipStream_t st);
+
+}  // namespace rsgpu

@@ -1,0 +1,764 @@
+// rs_kernels.hip -- MI355X (gfx950, CDNA4) kernels of the Reed-Solomon GF(2^8)
+// erasure engine.  Hot path of benchmark/isa_throughput: the GF dot product
+// that ISA-L computes with gf_{1..4}vect_dot_prod_avx2 (isa/gf_4vect_dot_prod_
+// avx2.asm:303-451, dispatched by ec_encode_data_avx2, isa/ec_highlevel_func.c:
+// 106-135) -- here as wavefront-wide byte arithmetic on the VALU.  No MFMA: the
+// work is byte-wise GF(2^8) multiply-accumulate, not a float contraction.
+//
+// Data layout in HBM: one row per symbol, rows of a block at a fixed pitch,
+// blocks back to back ([B][rows][pitch]).  A lane owns 4-byte columns of a row,
+// so every wave-wide load/store is a contiguous, coalesced 256-512 B segment.
+//
+// Kernels
+//   k_dot_generic<R>  out[r] = XOR_j c[r][j] * in[j] for RUNTIME coefficients
+//                     (decode matrices, arbitrary encode matrices).  Per
+//                     coefficient and dword: three v_perm_b32 8-entry lookups
+//                     (bits 0-2, 3-5, 6-7 of every byte) + 1.5 v_bitop3 XORs.
+//   k_rs_encode_lh<K,E> the gf_gen_rs_matrix (Vandermonde) encode with
+//                     COMPILE-TIME coefficients: per source dword the 16-entry
+//                     low/high nibble product tables L[n]=n*x, H[n]=(16n)*x are
+//                     built in registers once (7 xtimes + 22 XORs) and every
+//                     coefficient costs one v_bitop3 (acc ^= L[c&15] ^ H[c>>4]).
+//   k_decode_prepare  one workgroup per block: survivor rows -> k x k matrix
+//                     -> GF Gauss-Jordan inversion in LDS (isa/ec_base.c:99-152
+//                     semantics) -> decode rows -> v_perm tables + row pointers.
+//   k_fill_synth      seeded synthetic symbols (counter-based, see rs_synth.h).
+//   k_compare_rows    verify_data (isa.cpp:215-229) on the device.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <utility>
+
+#include "gf256.h"
+#include "rs_kernels.h"
+#include "rs_synth.h"
+
+namespace rsgpu {
+
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c)
+{
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+
+__device__ __forceinline__ uint32_t vperm(uint32_t hi, uint32_t lo, uint32_t sel)
+{
+    return __builtin_amdgcn_perm(hi, lo, sel);
+}
+
+// Row pointers fetched from memory are generic (flat) pointers; loads through
+// them would be flat_load (out-of-order vs LDS, forcing vmcnt(0)+lgkmcnt(0)
+// waits).  All rows live in global memory, so address-space-cast them.
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) const u32x4 g_cu32x4;
+typedef __attribute__((address_space(1))) u32x4 g_u32x4;
+__device__ __forceinline__ uint4 gload16(const uint8_t* p, long long w)
+{
+    const u32x4 v = ((g_cu32x4*)p)[w];
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void gstore16(uint8_t* p, long long w, uint4 v)
+{
+    u32x4 t;
+    t.x = v.x; t.y = v.y; t.z = v.z; t.w = v.w;
+    ((g_u32x4*)p)[w] = t;
+}
+
+// ---------------------------------------------------------------------------
+// Generic runtime-coefficient dot product
+// ---------------------------------------------------------------------------
+// Tables of one coefficient c (gf256.h perm_tables): four dwords
+// {c*{0..3}, c*{4..7}, c*{0,8,16,24}, c*{32..56}} for the bits 0-2 / 3-5
+// lookups (tabs4, uint4 per coefficient) and one dword c*{0,64,128,192} for
+// bits 6-7 (ctab).  Layout per block: [k][rows_pad].
+// srcs: [B][k] row pointers, dsts: [B][rows] row pointers (device memory).
+//
+// Each workgroup owns one block and a strided set of 16-byte columns; it
+// stages its block's R-row slice of tabs4 in LDS once (wave-uniform
+// ds_read_b128 broadcasts feed v_perm with VGPR operands, so the single
+// constant-bus slot is left for the ctab dword, read with s_load).  A lane
+// keeps 4 dwords x R rows of accumulators: per coefficient and dword the
+// cost is three v_perm + two XORs, and one LDS broadcast per 4 dwords.
+
+template <int R>
+__global__ __launch_bounds__(256) void k_dot_generic(const uint8_t* const* __restrict__ srcs,
+                                                     uint8_t* const* __restrict__ dsts,
+                                                     const uint4* __restrict__ tabs4,
+                                                     const uint32_t* __restrict__ ctab,
+                                                     long long tab_block_stride, int k, int rows,
+                                                     int rows_pad, int row0, long long n_ow,
+                                                     const int* __restrict__ status)
+{
+    extern __shared__ uint4 ltab[];  // [k][R]
+    const int b = blockIdx.y;
+    if (status != nullptr && status[b] != 0)
+        return;
+    const uint8_t* const* S = srcs + (size_t)b * k;
+    uint8_t* const* Dst = dsts + (size_t)b * rows;
+    const uint4* T4 = tabs4 + (size_t)b * tab_block_stride;
+    const uint32_t* TC = ctab + (size_t)b * tab_block_stride + row0;
+    const int nr = (rows - row0) < R ? (rows - row0) : R;
+
+    for (int idx = threadIdx.x; idx < k * R; idx += blockDim.x) {
+        const int j = idx / R, r = idx - j * R;
+        ltab[idx] = T4[(size_t)j * rows_pad + row0 + r];
+    }
+    __syncthreads();
+
+    for (long long w = (long long)blockIdx.x * blockDim.x + threadIdx.x; w < n_ow;
+         w += (long long)gridDim.x * blockDim.x) {
+        uint4 acc[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+            acc[r] = make_uint4(0, 0, 0, 0);
+        uint4 xn = gload16(S[0], w);
+        for (int j = 0; j < k; ++j) {
+            const uint4 x = xn;
+            if (j + 1 < k)
+                xn = gload16(S[j + 1], w);
+            const uint32_t s0x = x.x & 0x07070707u, s1x = (x.x >> 3) & 0x07070707u, s2x = (x.x >> 6) & 0x03030303u;
+            const uint32_t s0y = x.y & 0x07070707u, s1y = (x.y >> 3) & 0x07070707u, s2y = (x.y >> 6) & 0x03030303u;
+            const uint32_t s0z = x.z & 0x07070707u, s1z = (x.z >> 3) & 0x07070707u, s2z = (x.z >> 6) & 0x03030303u;
+            const uint32_t s0w = x.w & 0x07070707u, s1w = (x.w >> 3) & 0x07070707u, s2w = (x.w >> 6) & 0x03030303u;
+            const uint4* lt = ltab + j * R;
+            const uint32_t* ct = TC + (size_t)j * rows_pad;
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const uint4 t = lt[r];
+                const uint32_t c = ct[r];
+                acc[r].x = xor3(acc[r].x, vperm(t.y, t.x, s0x), vperm(t.w, t.z, s1x)) ^ vperm(c, c, s2x);
+                acc[r].y = xor3(acc[r].y, vperm(t.y, t.x, s0y), vperm(t.w, t.z, s1y)) ^ vperm(c, c, s2y);
+                acc[r].z = xor3(acc[r].z, vperm(t.y, t.x, s0z), vperm(t.w, t.z, s1z)) ^ vperm(c, c, s2z);
+                acc[r].w = xor3(acc[r].w, vperm(t.y, t.x, s0w), vperm(t.w, t.z, s1w)) ^ vperm(c, c, s2w);
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+            if (r < nr)
+                gstore16(Dst[row0 + r], w, acc[r]);
+    }
+}
+
+// Byte-granular variant for unaligned pointers or the len % 16 tail: each
+// thread produces one byte with the same three lookups.
+__global__ __launch_bounds__(256) void k_dot_bytes(const uint8_t* const* __restrict__ srcs,
+                                                   uint8_t* const* __restrict__ dsts,
+                                                   const uint4* __restrict__ tabs4,
+                                                   const uint32_t* __restrict__ ctab,
+                                                   long long tab_block_stride, int k, int rows,
+                                                   int rows_pad, long long first, long long len,
+                                                   const int* __restrict__ status)
+{
+    const int b = blockIdx.y;
+    if (status != nullptr && status[b] != 0)
+        return;
+    const long long i = first + (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= len)
+        return;
+    const uint8_t* const* S = srcs + (size_t)b * k;
+    uint8_t* const* Dst = dsts + (size_t)b * rows;
+    const uint4* T4 = tabs4 + (size_t)b * tab_block_stride;
+    const uint32_t* TC = ctab + (size_t)b * tab_block_stride;
+    for (int r = 0; r < rows; ++r) {
+        uint32_t acc = 0;
+        for (int j = 0; j < k; ++j) {
+            const uint32_t x = S[j][i];
+            const uint4 t = T4[(size_t)j * rows_pad + r];
+            const uint32_t c = TC[(size_t)j * rows_pad + r];
+            acc ^= vperm(t.y, t.x, x & 7u) ^ vperm(t.w, t.z, (x >> 3) & 7u) ^ vperm(c, c, (x >> 6) & 3u);
+        }
+        Dst[r][i] = (uint8_t)acc;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Compile-time-coefficient RS (gf_gen_rs_matrix) encode
+// ---------------------------------------------------------------------------
+
+template <int K, int E>
+struct VandCoefs {
+    uint8_t c[E][K];
+    // same recurrence as gf_gen_rs_matrix (isa/ec_base.c:71-78)
+    constexpr VandCoefs() : c()
+    {
+        uint8_t gen = 1;
+        for (int p = 0; p < E; ++p) {
+            uint8_t v = 1;
+            for (int j = 0; j < K; ++j) {
+                c[p][j] = v;
+                v = gf_mul_slow(v, gen);
+            }
+            gen = gf_mul_slow(gen, 2);
+        }
+    }
+};
+
+// x * 2 for the four bytes of a dword: shift, then fold the carried-out top
+// bits back in as 0x1D.  The fold multiply runs in 16-bit lanes
+// (v_pk_mul_lo_u16): each half holds two flag bits 8 apart, so 0x1D*flag
+// never carries across a byte.
+__device__ __forceinline__ uint32_t xtime4(uint32_t x)
+{
+    typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+    const uint32_t hi7 = (x >> 7) & 0x01010101u;
+    us2 h = __builtin_bit_cast(us2, hi7);
+    h = h * (us2){0x1d, 0x1d};
+    const uint32_t red = __builtin_bit_cast(uint32_t, h);
+    return ((x << 1) & 0xfefefefeu) ^ red;
+}
+
+template <int K, int E>
+struct VandHolder {
+    static constexpr VandCoefs<K, E> v{};
+};
+
+// acc ^= c*x from the nibble tables, c a compile-time constant
+template <int C>
+__device__ __forceinline__ void lh_mac(uint32_t& acc, const uint32_t (&Lt)[16],
+                                       const uint32_t (&Ht)[16])
+{
+    constexpr int lo = C & 15, hi = C >> 4;
+    if constexpr (lo != 0 && hi != 0)
+        acc = xor3(acc, Lt[lo], Ht[hi]);
+    else if constexpr (lo != 0)
+        acc ^= Lt[lo];
+    else if constexpr (hi != 0)
+        acc ^= Ht[hi];
+}
+
+template <int K, int E, int J, int... Rs>
+__device__ __forceinline__ void lh_rows(uint32_t (&acc)[E], const uint32_t (&Lt)[16],
+                                        const uint32_t (&Ht)[16],
+                                        std::integer_sequence<int, Rs...>)
+{
+    (lh_mac<VandHolder<K, E>::v.c[Rs][J]>(acc[Rs], Lt, Ht), ...);
+}
+
+// One source row J: build L/H for this dword, fold into all E parities.
+template <int K, int E, int J>
+__device__ __forceinline__ void lh_source(uint32_t (&acc)[E], uint32_t x)
+{
+    uint32_t bs[8];
+    bs[0] = x;
+#pragma unroll
+    for (int t = 1; t < 8; ++t)
+        bs[t] = xtime4(bs[t - 1]);
+    uint32_t Lt[16], Ht[16];
+    Lt[0] = 0;
+    Ht[0] = 0;
+#pragma unroll
+    for (int n = 1; n < 16; ++n) {
+        const int low = n & -n;
+        const int bit = low == 1 ? 0 : low == 2 ? 1 : low == 4 ? 2 : 3;
+        Lt[n] = (n == low) ? bs[bit] : (Lt[n ^ low] ^ bs[bit]);
+        Ht[n] = (n == low) ? bs[4 + bit] : (Ht[n ^ low] ^ bs[4 + bit]);
+    }
+    lh_rows<K, E, J>(acc, Lt, Ht, std::make_integer_sequence<int, E>{});
+}
+
+template <int K, int E, int J>
+__device__ __forceinline__ void lh_sources(uint32_t (&acc)[E], const uint8_t* sb, long long pitch,
+                                           long long w, uint32_t x)
+{
+    uint32_t xn = 0;
+    if constexpr (J + 1 < K)
+        xn = reinterpret_cast<const uint32_t*>(sb + (size_t)(J + 1) * pitch)[w];
+    lh_source<K, E, J>(acc, x);
+    if constexpr (J + 1 < K)
+        lh_sources<K, E, J + 1>(acc, sb, pitch, w, xn);
+}
+
+template <int K, int E>
+__global__ __launch_bounds__(256) void k_rs_encode_lh(const uint8_t* __restrict__ src,
+                                                      uint8_t* __restrict__ par, long long pitch,
+                                                      long long n_dw)
+{
+    const int b = blockIdx.y;
+    const uint8_t* sb = src + (size_t)b * K * pitch;
+    uint8_t* pb = par + (size_t)b * E * pitch;
+
+    for (long long w = (long long)blockIdx.x * blockDim.x + threadIdx.x; w < n_dw;
+         w += (long long)gridDim.x * blockDim.x) {
+        uint32_t acc[E];
+#pragma unroll
+        for (int r = 0; r < E; ++r)
+            acc[r] = 0;
+        const uint32_t x0 = reinterpret_cast<const uint32_t*>(sb)[w];
+        lh_sources<K, E, 0>(acc, sb, pitch, w, x0);
+#pragma unroll
+        for (int r = 0; r < E; ++r)
+            reinterpret_cast<uint32_t*>(pb + (size_t)r * pitch)[w] = acc[r];
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Decode preparation: one workgroup per block
+// ---------------------------------------------------------------------------
+// err:    [B][e] erased ORIGINAL indices, ascending (isa.cpp:150-153)
+// Produces per block: status (0 / -1 singular), survivor row pointers [k],
+// output row pointers [e], v_perm tables [k][rows_pad][5] of the decode rows
+// c[i][j] = inv(b)[err[i]][j] (isa.cpp:177-204).
+// LDS: two k x k byte matrices + log/antilog tables.
+
+__global__ __launch_bounds__(256) void k_decode_prepare(int k, int e, int rows_pad,
+                                                        const uint8_t* __restrict__ err,
+                                                        const uint8_t* src, long long src_pitch,
+                                                        const uint8_t* par, long long par_pitch,
+                                                        uint8_t* out, long long out_pitch,
+                                                        const uint8_t** surv_ptrs,
+                                                        uint8_t** out_ptrs, uint4* tabs4,
+                                                        uint32_t* ctab, long long tab_block_stride,
+                                                        int* status)
+{
+    extern __shared__ __align__(16) uint8_t lds[];
+    uint8_t* gexp = lds;             // 512
+    uint8_t* glog = lds + 512;       // 256
+    uint8_t* in_err = lds + 768;     // 256
+    uint8_t* surv = lds + 1024;      // 256
+    int* sh = reinterpret_cast<int*>(lds + 1280);  // 16 ints
+    uint8_t* A = lds + 1344;         // k*k
+    uint8_t* Dm = A + k * k;         // k*k
+
+    const int b = blockIdx.x;
+    const int tid = threadIdx.x, nt = blockDim.x;
+    const int m = k + e;
+
+    if (tid == 0) {
+        unsigned v = 1;
+        for (int i = 0; i < 255; ++i) {
+            gexp[i] = (uint8_t)v;
+            gexp[i + 255] = (uint8_t)v;
+            glog[v] = (uint8_t)i;
+            v <<= 1;
+            if (v & 0x100)
+                v ^= 0x11D;
+        }
+        gexp[510] = gexp[0];
+        gexp[511] = gexp[1];
+        glog[0] = 0;
+    }
+    for (int i = tid; i < 256; i += nt)
+        in_err[i] = 0;
+    __syncthreads();
+    const uint8_t* eb = err + (size_t)b * e;
+    for (int i = tid; i < e; i += nt)
+        in_err[eb[i]] = 1;
+    __syncthreads();
+    if (tid == 0) {
+        // survivors: ascending encode-row index skipping erased (isa.cpp:177-182)
+        int r = 0, bad = 0;
+        for (int i = 0; i < k; ++i, ++r) {
+            while (r < m && in_err[r])
+                ++r;
+            if (r >= m) {  // malformed erasure list (duplicates / out of range)
+                bad = 1;
+                r = 0;
+            }
+            surv[i] = (uint8_t)r;
+        }
+        for (int i = 0; i < e; ++i)
+            bad |= (eb[i] >= k);
+        sh[0] = bad ? -2 : 0;
+    }
+    __syncthreads();
+    if (sh[0] != 0) {
+        if (tid == 0)
+            status[b] = sh[0];
+        return;
+    }
+    // b[i][j] = a[surv[i]][j], a = gf_gen_rs_matrix(m, k)
+    for (int idx = tid; idx < k * k; idx += nt) {
+        const int i = idx / k, j = idx - i * k;
+        const int r = surv[i];
+        uint8_t v;
+        if (r < k)
+            v = (r == j) ? 1 : 0;
+        else {
+            const int p = r - k;
+            v = gexp[(p * j) % 255];
+        }
+        A[idx] = v;
+        Dm[idx] = (i == j) ? 1 : 0;
+    }
+    __syncthreads();
+    auto gmul = [&](uint8_t x, uint8_t y) -> uint8_t {
+        return (x && y) ? gexp[glog[x] + glog[y]] : (uint8_t)0;
+    };
+    // Gauss-Jordan (isa/ec_base.c:99-152): zero pivot -> swap with the first
+    // lower row holding a non-zero in that column; singular -> -1.
+    for (int i = 0; i < k; ++i) {
+        if (tid == 0) {
+            int piv = i;
+            if (A[i * k + i] == 0) {
+                piv = -1;
+                for (int j = i + 1; j < k; ++j)
+                    if (A[j * k + i]) {
+                        piv = j;
+                        break;
+                    }
+            }
+            sh[1] = piv;
+        }
+        __syncthreads();
+        const int piv = sh[1];
+        if (piv < 0) {
+            if (tid == 0)
+                sh[0] = -1;
+            break;
+        }
+        if (piv != i) {
+            for (int c = tid; c < k; c += nt) {
+                uint8_t t = A[i * k + c];
+                A[i * k + c] = A[piv * k + c];
+                A[piv * k + c] = t;
+                t = Dm[i * k + c];
+                Dm[i * k + c] = Dm[piv * k + c];
+                Dm[piv * k + c] = t;
+            }
+            __syncthreads();
+        }
+        const uint8_t pinv = gexp[255 - glog[A[i * k + i]]];
+        __syncthreads();
+        for (int c = tid; c < k; c += nt) {
+            A[i * k + c] = gmul(A[i * k + c], pinv);
+            Dm[i * k + c] = gmul(Dm[i * k + c], pinv);
+        }
+        __syncthreads();
+        // eliminate column i from every other row; factor read before update
+        for (int idx = tid; idx < k * k; idx += nt) {
+            const int r = idx / k, c = idx - r * k;
+            if (r == i)
+                continue;
+            const uint8_t f = A[r * k + i];
+            if (c == i)
+                continue;  // column i updated after the sweep
+            A[idx] ^= gmul(f, A[i * k + c]);
+            Dm[idx] ^= gmul(f, Dm[i * k + c]);
+        }
+        __syncthreads();
+        for (int r = tid; r < k; r += nt) {
+            if (r == i)
+                continue;
+            const uint8_t f = A[r * k + i];
+            // column i of Dm was handled in the sweep only for c != i
+            Dm[r * k + i] ^= gmul(f, Dm[i * k + i]);
+            A[r * k + i] = 0;
+        }
+        __syncthreads();
+    }
+    __syncthreads();
+    const int st = sh[0];
+    if (tid == 0)
+        status[b] = st;
+    // pointers: survivors from the encoder's data / parity rows, outputs
+    for (int i = tid; i < k; i += nt) {
+        const int r = surv[i];
+        surv_ptrs[(size_t)b * k + i] = (r < k) ? src + ((size_t)b * k + r) * src_pitch
+                                               : par + ((size_t)b * e + (r - k)) * par_pitch;
+    }
+    for (int i = tid; i < e; i += nt)
+        out_ptrs[(size_t)b * e + i] = out + ((size_t)b * e + i) * out_pitch;
+    if (st != 0)
+        return;
+    // tables: [j][rows_pad], rows beyond e zero
+    uint4* t4 = tabs4 + (size_t)b * tab_block_stride;
+    uint32_t* tc = ctab + (size_t)b * tab_block_stride;
+    for (int idx = tid; idx < k * rows_pad; idx += nt) {
+        const int j = idx / rows_pad, r = idx - j * rows_pad;
+        uint32_t t[5] = {0, 0, 0, 0, 0};
+        if (r < e) {
+            const uint8_t c = Dm[eb[r] * k + j];
+            uint8_t v[20];
+#pragma unroll
+            for (int n = 0; n < 8; ++n) {
+                v[n] = gmul(c, (uint8_t)n);
+                v[8 + n] = gmul(c, (uint8_t)(n << 3));
+            }
+#pragma unroll
+            for (int n = 0; n < 4; ++n)
+                v[16 + n] = gmul(c, (uint8_t)(n << 6));
+#pragma unroll
+            for (int q = 0; q < 5; ++q)
+                t[q] = (uint32_t)v[4 * q] | ((uint32_t)v[4 * q + 1] << 8) |
+                       ((uint32_t)v[4 * q + 2] << 16) | ((uint32_t)v[4 * q + 3] << 24);
+        }
+        t4[idx] = make_uint4(t[0], t[1], t[2], t[3]);
+        tc[idx] = t[4];
+    }
+    (void)m;
+}
+
+// ---------------------------------------------------------------------------
+// Synthetic data and verification
+// ---------------------------------------------------------------------------
+
+__global__ __launch_bounds__(256) void k_fill_synth(uint8_t* __restrict__ dst, long long rows,
+                                                    long long len, long long pitch,
+                                                    unsigned long long seed,
+                                                    unsigned long long row0)
+{
+    const long long words = (len + 7) / 8;
+    const long long total = rows * words;
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+         i += (long long)gridDim.x * blockDim.x) {
+        const long long r = i / words, w = i - r * words;
+        const uint64_t v = synth_word(seed, row0 + (uint64_t)r, (uint64_t)w);
+        uint8_t* p = dst + r * pitch + w * 8;
+        if (w * 8 + 8 <= len && ((reinterpret_cast<uintptr_t>(p) & 7) == 0)) {
+            *reinterpret_cast<uint64_t*>(p) = v;
+        } else {
+            for (int q = 0; q < 8 && w * 8 + q < len; ++q)
+                p[q] = (uint8_t)(v >> (8 * q));
+        }
+    }
+}
+
+// mismatches[b] += number of differing bytes between recovered row i of block
+// b and the original row err[b][i] of that block.
+__global__ __launch_bounds__(256) void k_compare_rows(const uint8_t* __restrict__ src,
+                                                      long long src_pitch, int k,
+                                                      const uint8_t* __restrict__ out,
+                                                      long long out_pitch, int e,
+                                                      const uint8_t* __restrict__ err,
+                                                      long long len,
+                                                      unsigned long long* __restrict__ mismatches)
+{
+    const int b = blockIdx.z, i = blockIdx.y;
+    const uint8_t* o = out + ((size_t)b * e + i) * out_pitch;
+    const int sidx = err[(size_t)b * e + i];
+    if (sidx >= k) {  // not an original: count the whole row as unverifiable
+        if (blockIdx.x == 0 && threadIdx.x == 0)
+            atomicAdd(&mismatches[b], (unsigned long long)len);
+        return;
+    }
+    const uint8_t* s = src + ((size_t)b * k + sidx) * src_pitch;
+    unsigned long long bad = 0;
+    for (long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x; p < len;
+         p += (long long)gridDim.x * blockDim.x)
+        bad += (o[p] != s[p]);
+    // wave reduction then one atomic per wave
+    for (int off = 32; off > 0; off >>= 1)
+        bad += __shfl_down(bad, off, 64);
+    if ((threadIdx.x & 63) == 0 && bad)
+        atomicAdd(&mismatches[b], bad);
+}
+
+// ---------------------------------------------------------------------------
+// Host launch wrappers (declared in rs_kernels.h)
+// ---------------------------------------------------------------------------
+
+template <int R>
+static hipError_t launch_generic_R(const DotArgs& a, hipStream_t st)
+{
+    const long long n_ow = a.len / 16;
+    if (n_ow > 0) {
+        const size_t lds = (size_t)a.k * R * sizeof(uint4);
+        static bool attr_set = false;
+        if (!attr_set) {
+            (void)hipFuncSetAttribute((const void*)k_dot_generic<R>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+            attr_set = true;
+        }
+        long long per_block = (n_ow + 255) / 256;
+        long long fill = (2048 + a.blocks - 1) / a.blocks;
+        long long gx = per_block < fill ? per_block : fill;
+        if (gx < 1)
+            gx = 1;
+        dim3 grid((unsigned)gx, (unsigned)a.blocks);
+        for (int row0 = 0; row0 < a.rows; row0 += R) {
+            hipLaunchKernelGGL(k_dot_generic<R>, grid, dim3(256), lds, st, a.srcs, a.dsts, a.tabs4,
+                               a.ctab, a.tab_block_stride, a.k, a.rows, a.rows_pad, row0, n_ow,
+                               a.status);
+        }
+    }
+    const long long first = n_ow * 16;
+    if (first < a.len) {
+        const long long nb = a.len - first;
+        dim3 grid((unsigned)((nb + 255) / 256), (unsigned)a.blocks);
+        hipLaunchKernelGGL(k_dot_bytes, grid, dim3(256), 0, st, a.srcs, a.dsts, a.tabs4, a.ctab,
+                           a.tab_block_stride, a.k, a.rows, a.rows_pad, first, a.len, a.status);
+    }
+    return hipGetLastError();
+}
+
+int generic_rows_per_pass(int rows)
+{
+    static const int Rs[] = {1, 2, 4, 8, 12, 16, 20, 24, 32};
+    const int want = rows < 32 ? rows : 32;
+    for (int r : Rs)
+        if (r >= want)
+            return r;
+    return 32;
+}
+
+hipError_t launch_dot_generic(const DotArgs& a, hipStream_t st)
+{
+    if (a.bytewise) {
+        dim3 grid((unsigned)((a.len + 255) / 256), (unsigned)a.blocks);
+        hipLaunchKernelGGL(k_dot_bytes, grid, dim3(256), 0, st, a.srcs, a.dsts, a.tabs4, a.ctab,
+                           a.tab_block_stride, a.k, a.rows, a.rows_pad, 0LL, a.len, a.status);
+        return hipGetLastError();
+    }
+    switch (generic_rows_per_pass(a.rows)) {
+    case 1: return launch_generic_R<1>(a, st);
+    case 2: return launch_generic_R<2>(a, st);
+    case 4: return launch_generic_R<4>(a, st);
+    case 8: return launch_generic_R<8>(a, st);
+    case 12: return launch_generic_R<12>(a, st);
+    case 16: return launch_generic_R<16>(a, st);
+    case 20: return launch_generic_R<20>(a, st);
+    case 24: return launch_generic_R<24>(a, st);
+    default: return launch_generic_R<32>(a, st);
+    }
+}
+
+template <int K, int E>
+static hipError_t launch_lh(const uint8_t* src, uint8_t* par, long long pitch, long long len,
+                            long long blocks, hipStream_t st)
+{
+    const long long n_dw = len / 4;
+    const long long want = (n_dw + 255) / 256;
+    const long long cap = 65535;
+    dim3 grid((unsigned)(want < cap ? want : cap), (unsigned)blocks);
+    hipLaunchKernelGGL((k_rs_encode_lh<K, E>), grid, dim3(256), 0, st, src, par, pitch, n_dw);
+    return hipGetLastError();
+}
+
+bool rs_encode_specialized_available(int k, int e)
+{
+    return (k == 16 && e == 4) || (k == 16 && e == 8) || (k == 64 && e == 32) ||
+           (k == 100 && e == 20) || (k == 5 && e == 4);
+}
+
+hipError_t launch_rs_encode_specialized(int k, int e, const uint8_t* src, uint8_t* par,
+                                        long long pitch, long long len, long long blocks,
+                                        hipStream_t st)
+{
+    if (k == 16 && e == 4) return launch_lh<16, 4>(src, par, pitch, len, blocks, st);
+    if (k == 16 && e == 8) return launch_lh<16, 8>(src, par, pitch, len, blocks, st);
+    if (k == 64 && e == 32) return launch_lh<64, 32>(src, par, pitch, len, blocks, st);
+    if (k == 100 && e == 20) return launch_lh<100, 20>(src, par, pitch, len, blocks, st);
+    if (k == 5 && e == 4) return launch_lh<5, 4>(src, par, pitch, len, blocks, st);
+    return hipErrorInvalidValue;
+}
+
+size_t decode_prepare_lds_bytes(int k) { return 1344 + 2 * (size_t)k * k; }
+
+hipError_t launch_decode_prepare(const PrepArgs& a, hipStream_t st)
+{
+    const size_t lds = decode_prepare_lds_bytes(a.k);
+    static bool attr_set = false;
+    if (!attr_set) {
+        (void)hipFuncSetAttribute((const void*)k_decode_prepare,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        attr_set = true;
+    }
+    hipLaunchKernelGGL(k_decode_prepare, dim3((unsigned)a.blocks), dim3(256), lds, st, a.k, a.e,
+                       a.rows_pad, a.err, a.src, a.src_pitch, a.par, a.par_pitch, a.out,
+                       a.out_pitch, a.surv_ptrs, a.out_ptrs, a.tabs4, a.ctab,
+                       a.tab_block_stride, a.status);
+    return hipGetLastError();
+}
+
+hipError_t launch_fill_synth(uint8_t* dst, long long rows, long long len, long long pitch,
+                             unsigned long long seed, unsigned long long row0, hipStream_t st)
+{
+    const long long words = (len + 7) / 8;
+    const long long total = rows * words;
+    long long want = (total + 255) / 256;
+    if (want > 65536)
+        want = 65536;
+    if (want < 1)
+        want = 1;
+    hipLaunchKernelGGL(k_fill_synth, dim3((unsigned)want), dim3(256), 0, st, dst, rows, len,
+                       pitch, seed, row0);
+    return hipGetLastError();
+}
+
+hipError_t launch_compare_rows(const uint8_t* src, long long src_pitch, int k, const uint8_t* out,
+                               long long out_pitch, int e, const uint8_t* err, long long len,
+                               long long blocks, unsigned long long* mismatches, hipStream_t st)
+{
+    long long want = (len + 255) / 256;
+    if (want > 64)
+        want = 64;
+    if (want < 1)
+        want = 1;
+    dim3 grid((unsigned)want, (unsigned)e, (unsigned)blocks);
+    hipLaunchKernelGGL(k_compare_rows, grid, dim3(256), 0, st, src, src_pitch, k, out, out_pitch,
+                       e, err, len, mismatches);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Row pointer tables and the single-source update (ec_encode_data_update)
+// ---------------------------------------------------------------------------
+
+// out[b][r] = base + (b*rows_per_block + r)*pitch
+__global__ __launch_bounds__(256) void k_row_ptrs(const uint8_t* base, long long pitch,
+                                                  int rows_per_block, long long blocks,
+                                                  const uint8_t** out)
+{
+    const long long n = blocks * rows_per_block;
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (long long)gridDim.x * blockDim.x)
+        out[i] = base + i * pitch;
+}
+
+// coding[r][i] ^= c_r * data[i]  (isa/ec_base.c:307-321 semantics); tables as
+// the generic kernel: tabs4/ctab [rows] of the column vec_i.
+__global__ __launch_bounds__(256) void k_update(const uint8_t* __restrict__ data,
+                                                uint8_t* const* __restrict__ coding,
+                                                const uint4* __restrict__ tabs4,
+                                                const uint32_t* __restrict__ ctab, long long len)
+{
+    const int r = blockIdx.y;
+    const uint4 t = tabs4[r];
+    const uint32_t c = ctab[r];
+    uint8_t* out = coding[r];
+    const bool vec = ((reinterpret_cast<uintptr_t>(data) | reinterpret_cast<uintptr_t>(out)) & 15) == 0;
+    const long long n_ow = vec ? len / 16 : 0;
+    for (long long w = (long long)blockIdx.x * blockDim.x + threadIdx.x; w < n_ow;
+         w += (long long)gridDim.x * blockDim.x) {
+        const uint4 x = gload16(data, w);
+        uint4 o = gload16(out, w);
+        o.x ^= vperm(t.y, t.x, x.x & 0x07070707u) ^ vperm(t.w, t.z, (x.x >> 3) & 0x07070707u) ^ vperm(c, c, (x.x >> 6) & 0x03030303u);
+        o.y ^= vperm(t.y, t.x, x.y & 0x07070707u) ^ vperm(t.w, t.z, (x.y >> 3) & 0x07070707u) ^ vperm(c, c, (x.y >> 6) & 0x03030303u);
+        o.z ^= vperm(t.y, t.x, x.z & 0x07070707u) ^ vperm(t.w, t.z, (x.z >> 3) & 0x07070707u) ^ vperm(c, c, (x.z >> 6) & 0x03030303u);
+        o.w ^= vperm(t.y, t.x, x.w & 0x07070707u) ^ vperm(t.w, t.z, (x.w >> 3) & 0x07070707u) ^ vperm(c, c, (x.w >> 6) & 0x03030303u);
+        gstore16(out, w, o);
+    }
+    for (long long i = n_ow * 16 + (long long)blockIdx.x * blockDim.x + threadIdx.x; i < len;
+         i += (long long)gridDim.x * blockDim.x) {
+        const uint32_t x = data[i];
+        out[i] ^= (uint8_t)(vperm(t.y, t.x, x & 7u) ^ vperm(t.w, t.z, (x >> 3) & 7u) ^ vperm(c, c, (x >> 6) & 3u));
+    }
+}
+
+hipError_t launch_row_ptrs(const uint8_t* base, long long pitch, int rows_per_block,
+                           long long blocks, const uint8_t** out, hipStream_t st)
+{
+    long long n = blocks * rows_per_block;
+    long long g = (n + 255) / 256;
+    if (g > 4096)
+        g = 4096;
+    if (g < 1)
+        g = 1;
+    hipLaunchKernelGGL(k_row_ptrs, dim3((unsigned)g), dim3(256), 0, st, base, pitch,
+                       rows_per_block, blocks, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_update(const uint8_t* data, uint8_t* const* coding, const uint4* tabs4,
+                         const uint32_t* ctab, int rows, long long len, hipStream_t st)
+{
+    long long g = (len / 16 + 255) / 256;
+    if (g > 1024)
+        g = 1024;
+    if (g < 1)
+        g = 1;
+    hipLaunchKernelGGL(k_update, dim3((unsigned)g, (unsigned)rows), dim3(256), 0, st, data,
+                       coding, tabs4, ctab, len);
+    return hipGetLastError();
+}
+
+}  // namespace rsgpu

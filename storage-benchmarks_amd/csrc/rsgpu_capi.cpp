@@ -1,0 +1,653 @@
+// rsgpu_capi.cpp -- C ABI of librsgpu (include/rsgpu.h): host GF helpers with
+// ISA-L semantics, context/stream management, and the launch sequences of the
+// batched encode / decode hot path.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/rsgpu.h"
+#include "gf256.h"
+#include "rs_kernels.h"
+#include "rs_synth.h"
+
+struct rsgpu_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+    // grow-only device scratch for pointer tables / coefficient tables
+    void* d_scratch = nullptr;
+    size_t scratch_bytes = 0;
+    // pinned host staging for small uploads, guarded by an event
+    void* h_stage = nullptr;
+    size_t stage_bytes = 0;
+    hipEvent_t stage_done = nullptr;
+    bool stage_pending = false;
+};
+
+namespace {
+
+using namespace rsgpu;
+
+const GfTables& host_gf()
+{
+    static GfTables t = [] {
+        GfTables x{};
+        gf_build_tables(x);
+        return x;
+    }();
+    return t;
+}
+
+inline uint8_t hmul(uint8_t a, uint8_t b)
+{
+    const GfTables& t = host_gf();
+    return (a && b) ? t.exp[t.log[a] + t.log[b]] : 0;
+}
+
+int fail(rsgpu_ctx* ctx, int code, const std::string& msg)
+{
+    if (ctx)
+        ctx->err = msg;
+    return code;
+}
+
+#define RS_HIP(ctx, call)                                                                     \
+    do {                                                                                      \
+        hipError_t e_ = (call);                                                               \
+        if (e_ != hipSuccess)                                                                 \
+            return fail((ctx), RSGPU_ERR_HIP,                                                 \
+                        std::string(#call) + ": " + hipGetErrorString(e_));                   \
+    } while (0)
+
+int ensure_scratch(rsgpu_ctx* ctx, size_t bytes)
+{
+    if (ctx->scratch_bytes >= bytes)
+        return RSGPU_OK;
+    if (ctx->d_scratch) {
+        RS_HIP(ctx, hipStreamSynchronize(ctx->stream));
+        RS_HIP(ctx, hipFree(ctx->d_scratch));
+        ctx->d_scratch = nullptr;
+        ctx->scratch_bytes = 0;
+    }
+    size_t want = bytes < (1u << 20) ? (1u << 20) : bytes;
+    RS_HIP(ctx, hipMalloc(&ctx->d_scratch, want));
+    ctx->scratch_bytes = want;
+    return RSGPU_OK;
+}
+
+// Returns a pinned staging pointer of >= bytes, after the previous upload
+// from it has completed.
+int get_stage(rsgpu_ctx* ctx, size_t bytes, void** out)
+{
+    if (ctx->stage_pending) {
+        RS_HIP(ctx, hipEventSynchronize(ctx->stage_done));
+        ctx->stage_pending = false;
+    }
+    if (ctx->stage_bytes < bytes) {
+        if (ctx->h_stage)
+            RS_HIP(ctx, hipHostFree(ctx->h_stage));
+        size_t want = bytes < (1u << 20) ? (1u << 20) : bytes;
+        RS_HIP(ctx, hipHostMalloc(&ctx->h_stage, want));
+        ctx->stage_bytes = want;
+    }
+    *out = ctx->h_stage;
+    return RSGPU_OK;
+}
+
+int upload(rsgpu_ctx* ctx, void* d_dst, size_t bytes)
+{
+    RS_HIP(ctx, hipMemcpyAsync(d_dst, ctx->h_stage, bytes, hipMemcpyHostToDevice, ctx->stream));
+    RS_HIP(ctx, hipEventRecord(ctx->stage_done, ctx->stream));
+    ctx->stage_pending = true;
+    return RSGPU_OK;
+}
+
+inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+// Fill host tables [k][rows_pad] for coefficient matrix coef[rows][k]
+// (coef row r column j at coef[r*k + j]).
+void fill_tables(const uint8_t* coef, int k, int rows, int rows_pad, uint4* t4, uint32_t* tc)
+{
+    for (int j = 0; j < k; ++j)
+        for (int r = 0; r < rows_pad; ++r) {
+            uint32_t t[5] = {0, 0, 0, 0, 0};
+            if (r < rows)
+                perm_tables(coef[(size_t)r * k + j], t);
+            t4[(size_t)j * rows_pad + r] = make_uint4(t[0], t[1], t[2], t[3]);
+            tc[(size_t)j * rows_pad + r] = t[4];
+        }
+}
+
+int rows_pad_for(int rows)
+{
+    const int R = generic_rows_per_pass(rows);
+    return (rows + R - 1) / R * R;
+}
+
+// Generic dot product launch from HOST coefficients coef[rows][k] over
+// device pointer tables already in place (d_srcs [blocks][k], d_dsts
+// [blocks][rows]).  Uploads the tables into scratch at offset `tab_off`.
+int generic_from_host_coef(rsgpu_ctx* ctx, const uint8_t* coef, int k, int rows, long long len,
+                           long long blocks, const uint8_t* const* d_srcs, uint8_t* const* d_dsts,
+                           size_t tab_off, bool bytewise)
+{
+    const int rows_pad = rows_pad_for(rows);
+    const size_t n = (size_t)k * rows_pad;
+    const size_t bytes4 = n * sizeof(uint4), bytesc = n * sizeof(uint32_t);
+    void* stage;
+    int rc = get_stage(ctx, bytes4 + bytesc, &stage);
+    if (rc)
+        return rc;
+    uint4* t4 = (uint4*)stage;
+    uint32_t* tc = (uint32_t*)((char*)stage + bytes4);
+    fill_tables(coef, k, rows, rows_pad, t4, tc);
+    char* d = (char*)ctx->d_scratch + tab_off;
+    rc = upload(ctx, d, bytes4 + bytesc);
+    if (rc)
+        return rc;
+    DotArgs a{};
+    a.srcs = d_srcs;
+    a.dsts = d_dsts;
+    a.tabs4 = (const uint4*)d;
+    a.ctab = (const uint32_t*)(d + bytes4);
+    a.tab_block_stride = 0;
+    a.k = k;
+    a.rows = rows;
+    a.rows_pad = rows_pad;
+    a.len = len;
+    a.blocks = blocks;
+    a.status = nullptr;
+    a.bytewise = bytewise;
+    RS_HIP(ctx, launch_dot_generic(a, ctx->stream));
+    return RSGPU_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* rsgpu_version(void) { return "0.1.0"; }
+
+int rsgpu_create(int device, rsgpu_ctx** out)
+{
+    if (!out)
+        return RSGPU_ERR_ARG;
+    *out = nullptr;
+    if (hipSetDevice(device) != hipSuccess)
+        return RSGPU_ERR_HIP;
+    rsgpu_ctx* c = new rsgpu_ctx();
+    c->device = device;
+    if (hipEventCreateWithFlags(&c->stage_done, hipEventDisableTiming) != hipSuccess) {
+        delete c;
+        return RSGPU_ERR_HIP;
+    }
+    *out = c;
+    return RSGPU_OK;
+}
+
+int rsgpu_destroy(rsgpu_ctx* ctx)
+{
+    if (!ctx)
+        return RSGPU_ERR_ARG;
+    (void)hipSetDevice(ctx->device);
+    (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->d_scratch)
+        (void)hipFree(ctx->d_scratch);
+    if (ctx->h_stage)
+        (void)hipHostFree(ctx->h_stage);
+    if (ctx->stage_done)
+        (void)hipEventDestroy(ctx->stage_done);
+    delete ctx;
+    return RSGPU_OK;
+}
+
+int rsgpu_set_stream(rsgpu_ctx* ctx, void* s)
+{
+    if (!ctx)
+        return RSGPU_ERR_ARG;
+    ctx->stream = (hipStream_t)s;
+    return RSGPU_OK;
+}
+
+void* rsgpu_get_stream(rsgpu_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
+
+int rsgpu_synchronize(rsgpu_ctx* ctx)
+{
+    if (!ctx)
+        return RSGPU_ERR_ARG;
+    RS_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return RSGPU_OK;
+}
+
+const char* rsgpu_last_error(rsgpu_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int rsgpu_malloc(rsgpu_ctx* ctx, void** p, size_t bytes)
+{
+    if (!ctx || !p)
+        return RSGPU_ERR_ARG;
+    if (hipMalloc(p, bytes ? bytes : 1) != hipSuccess)
+        return fail(ctx, RSGPU_ERR_NOMEM, "hipMalloc failed");
+    return RSGPU_OK;
+}
+
+int rsgpu_free(rsgpu_ctx* ctx, void* p)
+{
+    if (!ctx)
+        return RSGPU_ERR_ARG;
+    RS_HIP(ctx, hipFree(p));
+    return RSGPU_OK;
+}
+
+int rsgpu_memcpy_h2d(rsgpu_ctx* ctx, void* dst, const void* src, size_t bytes)
+{
+    if (!ctx)
+        return RSGPU_ERR_ARG;
+    RS_HIP(ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ctx->stream));
+    RS_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return RSGPU_OK;
+}
+
+int rsgpu_memcpy_d2h(rsgpu_ctx* ctx, void* dst, const void* src, size_t bytes)
+{
+    if (!ctx)
+        return RSGPU_ERR_ARG;
+    RS_HIP(ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream));
+    RS_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return RSGPU_OK;
+}
+
+// ---- host GF helpers -------------------------------------------------------
+
+unsigned char rsgpu_gf_mul(unsigned char a, unsigned char b) { return hmul(a, b); }
+
+unsigned char rsgpu_gf_inv(unsigned char a)
+{
+    const GfTables& t = host_gf();
+    return a ? t.exp[255 - t.log[a]] : 0;
+}
+
+void rsgpu_gf_gen_rs_matrix(unsigned char* a, int m, int k)
+{
+    std::memset(a, 0, (size_t)m * k);
+    for (int i = 0; i < k; ++i)
+        a[(size_t)k * i + i] = 1;
+    uint8_t gen = 1;
+    for (int i = k; i < m; ++i) {
+        uint8_t p = 1;
+        for (int j = 0; j < k; ++j) {
+            a[(size_t)k * i + j] = p;
+            p = hmul(p, gen);
+        }
+        gen = hmul(gen, 2);
+    }
+}
+
+void rsgpu_gf_gen_cauchy1_matrix(unsigned char* a, int m, int k)
+{
+    std::memset(a, 0, (size_t)m * k);
+    for (int i = 0; i < k; ++i)
+        a[(size_t)k * i + i] = 1;
+    unsigned char* p = a + (size_t)k * k;
+    for (int i = k; i < m; ++i)
+        for (int j = 0; j < k; ++j)
+            *p++ = rsgpu_gf_inv((unsigned char)(i ^ j));
+}
+
+int rsgpu_gf_invert_matrix(unsigned char* in, unsigned char* out, const int n)
+{
+    std::memset(out, 0, (size_t)n * n);
+    for (int i = 0; i < n; ++i)
+        out[(size_t)i * n + i] = 1;
+    for (int i = 0; i < n; ++i) {
+        if (in[(size_t)i * n + i] == 0) {
+            int j = i + 1;
+            while (j < n && in[(size_t)j * n + i] == 0)
+                ++j;
+            if (j == n)
+                return -1;
+            for (int c = 0; c < n; ++c) {
+                std::swap(in[(size_t)i * n + c], in[(size_t)j * n + c]);
+                std::swap(out[(size_t)i * n + c], out[(size_t)j * n + c]);
+            }
+        }
+        const uint8_t piv = rsgpu_gf_inv(in[(size_t)i * n + i]);
+        for (int c = 0; c < n; ++c) {
+            in[(size_t)i * n + c] = hmul(in[(size_t)i * n + c], piv);
+            out[(size_t)i * n + c] = hmul(out[(size_t)i * n + c], piv);
+        }
+        for (int r = 0; r < n; ++r) {
+            if (r == i)
+                continue;
+            const uint8_t f = in[(size_t)r * n + i];
+            if (!f)
+                continue;
+            for (int c = 0; c < n; ++c) {
+                out[(size_t)r * n + c] ^= hmul(f, out[(size_t)i * n + c]);
+                in[(size_t)r * n + c] ^= hmul(f, in[(size_t)i * n + c]);
+            }
+        }
+    }
+    return 0;
+}
+
+void rsgpu_gf_vect_mul_init(unsigned char c, unsigned char* tbl)
+{
+    for (int x = 0; x < 16; ++x) {
+        tbl[x] = hmul(c, (uint8_t)x);
+        tbl[16 + x] = hmul(c, (uint8_t)(x << 4));
+    }
+}
+
+void rsgpu_ec_init_tables(int k, int rows, unsigned char* a, unsigned char* g)
+{
+    for (int i = 0; i < rows; ++i)
+        for (int j = 0; j < k; ++j) {
+            rsgpu_gf_vect_mul_init(*a++, g);
+            g += 32;
+        }
+}
+
+// ---- device, ISA-L-shaped ----------------------------------------------------
+
+int rsgpu_ec_encode_data(rsgpu_ctx* ctx, int len, int k, int rows, const unsigned char* gftbls,
+                         unsigned char** data, unsigned char** coding)
+{
+    if (!ctx || len < 0 || k <= 0 || rows < 0 || k > RSGPU_MAX_SOURCES || rows > 255 ||
+        (rows > 0 && (!gftbls || !data || !coding)))
+        return fail(ctx, RSGPU_ERR_ARG, "rsgpu_ec_encode_data: bad arguments");
+    if (rows == 0 || len == 0)
+        return RSGPU_OK;
+    // coefficient = tbl[1] of each 32-byte table (isa/ec_base.c:300)
+    std::vector<uint8_t> coef((size_t)rows * k);
+    for (int r = 0; r < rows; ++r)
+        for (int j = 0; j < k; ++j)
+            coef[(size_t)r * k + j] = gftbls[((size_t)r * k + j) * 32 + 1];
+    bool aligned = true;
+    for (int j = 0; j < k; ++j)
+        aligned &= ((uintptr_t)data[j] & 15) == 0;
+    for (int r = 0; r < rows; ++r)
+        aligned &= ((uintptr_t)coding[r] & 15) == 0;
+    const size_t ptr_bytes = align_up(sizeof(void*) * (size_t)(k + rows), 256);
+    const int rows_pad = rows_pad_for(rows);
+    const size_t tab_bytes = (size_t)k * rows_pad * (sizeof(uint4) + sizeof(uint32_t));
+    int rc = ensure_scratch(ctx, ptr_bytes + tab_bytes);
+    if (rc)
+        return rc;
+    // pointer tables go through the same staging buffer after the tables:
+    // stage layout [ptrs | tables] keeps one upload per call
+    void* stage;
+    rc = get_stage(ctx, ptr_bytes + tab_bytes, &stage);
+    if (rc)
+        return rc;
+    void** hp = (void**)stage;
+    for (int j = 0; j < k; ++j)
+        hp[j] = data[j];
+    for (int r = 0; r < rows; ++r)
+        hp[k + r] = coding[r];
+    uint4* t4 = (uint4*)((char*)stage + ptr_bytes);
+    uint32_t* tc = (uint32_t*)((char*)t4 + (size_t)k * rows_pad * sizeof(uint4));
+    fill_tables(coef.data(), k, rows, rows_pad, t4, tc);
+    rc = upload(ctx, ctx->d_scratch, ptr_bytes + tab_bytes);
+    if (rc)
+        return rc;
+    char* d = (char*)ctx->d_scratch;
+    DotArgs a{};
+    a.srcs = (const uint8_t* const*)d;
+    a.dsts = (uint8_t* const*)(d + sizeof(void*) * k);
+    a.tabs4 = (const uint4*)(d + ptr_bytes);
+    a.ctab = (const uint32_t*)(d + ptr_bytes + (size_t)k * rows_pad * sizeof(uint4));
+    a.tab_block_stride = 0;
+    a.k = k;
+    a.rows = rows;
+    a.rows_pad = rows_pad;
+    a.len = len;
+    a.blocks = 1;
+    a.status = nullptr;
+    a.bytewise = !aligned;
+    RS_HIP(ctx, launch_dot_generic(a, ctx->stream));
+    return RSGPU_OK;
+}
+
+int rsgpu_ec_encode_data_update(rsgpu_ctx* ctx, int len, int k, int rows, int vec_i,
+                                const unsigned char* gftbls, unsigned char* data,
+                                unsigned char** coding)
+{
+    if (!ctx || len < 0 || k <= 0 || rows < 0 || vec_i < 0 || vec_i >= k || rows > 255 ||
+        (rows > 0 && (!gftbls || !data || !coding)))
+        return fail(ctx, RSGPU_ERR_ARG, "rsgpu_ec_encode_data_update: bad arguments");
+    if (rows == 0 || len == 0)
+        return RSGPU_OK;
+    const size_t ptr_bytes = align_up(sizeof(void*) * (size_t)rows, 256);
+    const size_t tab_bytes = (size_t)rows * (sizeof(uint4) + sizeof(uint32_t));
+    int rc = ensure_scratch(ctx, ptr_bytes + tab_bytes);
+    if (rc)
+        return rc;
+    void* stage;
+    rc = get_stage(ctx, ptr_bytes + tab_bytes, &stage);
+    if (rc)
+        return rc;
+    void** hp = (void**)stage;
+    for (int r = 0; r < rows; ++r)
+        hp[r] = coding[r];
+    uint4* t4 = (uint4*)((char*)stage + ptr_bytes);
+    uint32_t* tc = (uint32_t*)((char*)t4 + (size_t)rows * sizeof(uint4));
+    for (int r = 0; r < rows; ++r) {
+        uint32_t t[5];
+        // coefficient of (row r, column vec_i): tbl[1] (isa/ec_base.c:316)
+        perm_tables(gftbls[((size_t)r * k + vec_i) * 32 + 1], t);
+        t4[r] = make_uint4(t[0], t[1], t[2], t[3]);
+        tc[r] = t[4];
+    }
+    rc = upload(ctx, ctx->d_scratch, ptr_bytes + tab_bytes);
+    if (rc)
+        return rc;
+    char* d = (char*)ctx->d_scratch;
+    RS_HIP(ctx, launch_update(data, (uint8_t* const*)d, (const uint4*)(d + ptr_bytes),
+                              (const uint32_t*)(d + ptr_bytes + (size_t)rows * sizeof(uint4)),
+                              rows, len, ctx->stream));
+    return RSGPU_OK;
+}
+
+// ---- device, batched -----------------------------------------------------------
+
+static int check_geom(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch, size_t blocks)
+{
+    if (!ctx)
+        return RSGPU_ERR_ARG;
+    if (k <= 0 || e < 0 || k + e > RSGPU_MAX_SOURCES || pitch < len || blocks == 0)
+        return fail(ctx, RSGPU_ERR_ARG, "bad geometry (k, e, len, pitch, blocks)");
+    return RSGPU_OK;
+}
+
+int rsgpu_encode_blocks(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch, size_t blocks,
+                        const unsigned char* d_src, unsigned char* d_parity,
+                        const unsigned char* coef)
+{
+    int rc = check_geom(ctx, k, e, len, pitch, blocks);
+    if (rc)
+        return rc;
+    if (e == 0 || len == 0)
+        return RSGPU_OK;
+    const bool aligned = ((uintptr_t)d_src % 16 == 0) && ((uintptr_t)d_parity % 16 == 0) &&
+                         (pitch % 16 == 0);
+    // Fast path: the gf_gen_rs_matrix code with compile-time coefficients.
+    if (!coef && aligned && len % 4 == 0 && rs_encode_specialized_available(k, e)) {
+        RS_HIP(ctx, launch_rs_encode_specialized(k, e, d_src, d_parity, (long long)pitch,
+                                                 (long long)len, (long long)blocks, ctx->stream));
+        return RSGPU_OK;
+    }
+    std::vector<uint8_t> c((size_t)e * k);
+    if (coef) {
+        std::memcpy(c.data(), coef, c.size());
+    } else {
+        std::vector<uint8_t> a((size_t)(k + e) * k);
+        rsgpu_gf_gen_rs_matrix(a.data(), k + e, k);
+        std::memcpy(c.data(), a.data() + (size_t)k * k, c.size());
+    }
+    const size_t src_ptr_bytes = align_up(sizeof(void*) * (size_t)k * blocks, 256);
+    const size_t dst_ptr_bytes = align_up(sizeof(void*) * (size_t)e * blocks, 256);
+    const int rows_pad = rows_pad_for(e);
+    const size_t tab_bytes = (size_t)k * rows_pad * (sizeof(uint4) + sizeof(uint32_t));
+    rc = ensure_scratch(ctx, src_ptr_bytes + dst_ptr_bytes + tab_bytes);
+    if (rc)
+        return rc;
+    char* d = (char*)ctx->d_scratch;
+    RS_HIP(ctx, launch_row_ptrs(d_src, (long long)pitch, k, (long long)blocks,
+                                (const uint8_t**)d, ctx->stream));
+    RS_HIP(ctx, launch_row_ptrs(d_parity, (long long)pitch, e, (long long)blocks,
+                                (const uint8_t**)(d + src_ptr_bytes), ctx->stream));
+    return generic_from_host_coef(ctx, c.data(), k, e, (long long)len, (long long)blocks,
+                                  (const uint8_t* const*)d, (uint8_t* const*)(d + src_ptr_bytes),
+                                  src_ptr_bytes + dst_ptr_bytes, !aligned);
+}
+
+static void decode_ws_layout(int k, int e, size_t blocks, size_t* off_surv, size_t* off_out,
+                             size_t* off_t4, size_t* off_tc, size_t* total)
+{
+    const int rows_pad = rows_pad_for(e);
+    size_t o = 0;
+    *off_surv = o;
+    o = align_up(o + sizeof(void*) * (size_t)k * blocks, 256);
+    *off_out = o;
+    o = align_up(o + sizeof(void*) * (size_t)e * blocks, 256);
+    *off_t4 = o;
+    o = align_up(o + sizeof(uint4) * (size_t)k * rows_pad * blocks, 256);
+    *off_tc = o;
+    o = align_up(o + sizeof(uint32_t) * (size_t)k * rows_pad * blocks, 256);
+    *total = o;
+}
+
+size_t rsgpu_decode_workspace_bytes(int k, int e, size_t blocks)
+{
+    if (k <= 0 || e <= 0)
+        return 256;
+    size_t a, b, c, d, t;
+    decode_ws_layout(k, e, blocks, &a, &b, &c, &d, &t);
+    return t;
+}
+
+int rsgpu_decode_prepare(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch, size_t blocks,
+                         const unsigned char* d_src, const unsigned char* d_parity,
+                         const unsigned char* d_err, unsigned char* d_out, void* d_workspace,
+                         int* d_status)
+{
+    int rc = check_geom(ctx, k, e, len, pitch, blocks);
+    if (rc)
+        return rc;
+    if (e == 0)
+        return RSGPU_OK;
+    if (e > k || !d_err || !d_workspace || !d_status)
+        return fail(ctx, RSGPU_ERR_ARG, "rsgpu_decode_prepare: bad arguments");
+    size_t o_surv, o_out, o_t4, o_tc, total;
+    decode_ws_layout(k, e, blocks, &o_surv, &o_out, &o_t4, &o_tc, &total);
+    char* ws = (char*)d_workspace;
+    const int rows_pad = rows_pad_for(e);
+    PrepArgs p{};
+    p.k = k;
+    p.e = e;
+    p.rows_pad = rows_pad;
+    p.blocks = (long long)blocks;
+    p.err = d_err;
+    p.src = d_src;
+    p.src_pitch = (long long)pitch;
+    p.par = d_parity;
+    p.par_pitch = (long long)pitch;
+    p.out = d_out;
+    p.out_pitch = (long long)pitch;
+    p.surv_ptrs = (const uint8_t**)(ws + o_surv);
+    p.out_ptrs = (uint8_t**)(ws + o_out);
+    p.tabs4 = (uint4*)(ws + o_t4);
+    p.ctab = (uint32_t*)(ws + o_tc);
+    p.tab_block_stride = (long long)k * rows_pad;
+    p.status = d_status;
+    RS_HIP(ctx, launch_decode_prepare(p, ctx->stream));
+    return RSGPU_OK;
+}
+
+int rsgpu_decode_apply(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch, size_t blocks,
+                       const unsigned char* d_src, const unsigned char* d_parity,
+                       unsigned char* d_out, void* d_workspace, const int* d_status)
+{
+    int rc = check_geom(ctx, k, e, len, pitch, blocks);
+    if (rc)
+        return rc;
+    if (e == 0 || len == 0)
+        return RSGPU_OK;
+    if (e > k || !d_workspace || !d_status)
+        return fail(ctx, RSGPU_ERR_ARG, "rsgpu_decode_apply: bad arguments");
+    size_t o_surv, o_out, o_t4, o_tc, total;
+    decode_ws_layout(k, e, blocks, &o_surv, &o_out, &o_t4, &o_tc, &total);
+    char* ws = (char*)d_workspace;
+    const int rows_pad = rows_pad_for(e);
+    const bool aligned = ((uintptr_t)d_src % 16 == 0) && ((uintptr_t)d_parity % 16 == 0) &&
+                         ((uintptr_t)d_out % 16 == 0) && (pitch % 16 == 0);
+    DotArgs a{};
+    a.srcs = (const uint8_t* const*)(ws + o_surv);
+    a.dsts = (uint8_t* const*)(ws + o_out);
+    a.tabs4 = (const uint4*)(ws + o_t4);
+    a.ctab = (const uint32_t*)(ws + o_tc);
+    a.tab_block_stride = (long long)k * rows_pad;
+    a.k = k;
+    a.rows = e;
+    a.rows_pad = rows_pad;
+    a.len = (long long)len;
+    a.blocks = (long long)blocks;
+    a.status = d_status;
+    a.bytewise = !aligned;
+    RS_HIP(ctx, launch_dot_generic(a, ctx->stream));
+    return RSGPU_OK;
+}
+
+int rsgpu_decode_blocks(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch, size_t blocks,
+                        const unsigned char* d_src, const unsigned char* d_parity,
+                        const unsigned char* d_err, unsigned char* d_out, void* d_workspace,
+                        int* d_status)
+{
+    int rc = rsgpu_decode_prepare(ctx, k, e, len, pitch, blocks, d_src, d_parity, d_err, d_out,
+                                  d_workspace, d_status);
+    if (rc)
+        return rc;
+    return rsgpu_decode_apply(ctx, k, e, len, pitch, blocks, d_src, d_parity, d_out, d_workspace,
+                              d_status);
+}
+
+int rsgpu_verify_blocks(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch, size_t blocks,
+                        const unsigned char* d_src, const unsigned char* d_out,
+                        const unsigned char* d_err, unsigned long long* d_mismatch)
+{
+    int rc = check_geom(ctx, k, e, len, pitch, blocks);
+    if (rc)
+        return rc;
+    if (e == 0 || len == 0)
+        return RSGPU_OK;
+    RS_HIP(ctx, launch_compare_rows(d_src, (long long)pitch, k, d_out, (long long)pitch, e, d_err,
+                                    (long long)len, (long long)blocks, d_mismatch, ctx->stream));
+    return RSGPU_OK;
+}
+
+int rsgpu_fill_synthetic(rsgpu_ctx* ctx, unsigned char* d_rows, size_t rows, size_t len,
+                         size_t pitch, uint64_t seed, uint64_t row0)
+{
+    if (!ctx || pitch < len)
+        return fail(ctx, RSGPU_ERR_ARG, "rsgpu_fill_synthetic: bad arguments");
+    if (rows == 0 || len == 0)
+        return RSGPU_OK;
+    RS_HIP(ctx, launch_fill_synth(d_rows, (long long)rows, (long long)len, (long long)pitch, seed,
+                                  row0, ctx->stream));
+    return RSGPU_OK;
+}
+
+int rsgpu_erasure_patterns(uint64_t seed, uint64_t blk0, size_t blocks, int k, int e,
+                           unsigned char* h_err)
+{
+    if (!h_err || k <= 0 || e < 0 || e > k || k > 256)
+        return RSGPU_ERR_ARG;
+    for (size_t b = 0; b < blocks; ++b)
+        erasure_pattern(seed, blk0 + b, k, e, h_err + b * (size_t)e);
+    return RSGPU_OK;
+}
+
+}  // extern "C"

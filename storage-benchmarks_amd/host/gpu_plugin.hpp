@@ -1,0 +1,154 @@
+// gpu_plugin.hpp -- gpu_encoder / gpu_decoder: MI355X peers of isa_encoder /
+// isa_decoder (benchmark/isa_throughput/isa.cpp:29-259) over the C ABI of
+// librsgpu (include/rsgpu.h).  One object carries `blocks` independent blocks
+// resident in HBM; blocks == 1 is exactly the reference's shape.
+#pragma once
+
+#include <cstdint>
+#include <cstdio>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "rsgpu.h"
+
+namespace sbamd {
+
+struct gpu_session {
+    rsgpu_ctx* ctx = nullptr;
+    explicit gpu_session(int device)
+    {
+        if (rsgpu_create(device, &ctx) != RSGPU_OK)
+            throw std::runtime_error("rsgpu_create failed (no HIP device?)");
+    }
+    ~gpu_session() { rsgpu_destroy(ctx); }
+    void check(int rc, const char* what) const
+    {
+        if (rc != RSGPU_OK)
+            throw std::runtime_error(std::string(what) + ": " + rsgpu_last_error(ctx));
+    }
+};
+
+inline size_t row_pitch(uint32_t symbol_size) { return (symbol_size + 255u) / 256u * 256u; }
+
+struct gpu_encoder {
+    gpu_encoder(std::shared_ptr<gpu_session> s, uint32_t symbols, uint32_t symbol_size,
+                uint32_t encoded_symbols, uint32_t blocks, uint64_t seed, uint64_t block0)
+        : m_s(std::move(s)), k(symbols), e(encoded_symbols), L(symbol_size), B(blocks),
+          pitch(row_pitch(symbol_size))
+    {
+        m_s->check(rsgpu_malloc(m_s->ctx, (void**)&src, (size_t)B * k * pitch), "alloc src");
+        m_s->check(rsgpu_malloc(m_s->ctx, (void**)&par, (size_t)B * (e ? e : 1) * pitch),
+                   "alloc parity");
+        // isa.cpp:55-58 fills originals with rand(); the seeded stream here
+        m_s->check(rsgpu_fill_synthetic(m_s->ctx, src, (size_t)B * k, L, pitch, seed, block0 * k),
+                   "fill");
+        m_s->check(rsgpu_synchronize(m_s->ctx), "sync");
+    }
+    ~gpu_encoder()
+    {
+        rsgpu_free(m_s->ctx, src);
+        rsgpu_free(m_s->ctx, par);
+    }
+    // isa.cpp:69-79: gf_gen_rs_matrix + ec_init_tables + ec_encode_data
+    void encode_all()
+    {
+        m_s->check(rsgpu_encode_blocks(m_s->ctx, (int)k, (int)e, L, pitch, B, src, par, nullptr),
+                   "rsgpu_encode_blocks");
+    }
+    void finish() { m_s->check(rsgpu_synchronize(m_s->ctx), "sync"); }
+    uint32_t block_size() const { return k * L; }
+    uint32_t symbol_size() const { return L; }
+    uint32_t payload_size() const { return L; }
+    uint32_t payload_count() const { return e; }
+    uint32_t blocks() const { return B; }
+
+    std::shared_ptr<gpu_session> m_s;
+    uint32_t k, e, L, B;
+    size_t pitch;
+    unsigned char* src = nullptr;
+    unsigned char* par = nullptr;
+};
+
+struct gpu_decoder {
+    gpu_decoder(std::shared_ptr<gpu_session> s, uint32_t symbols, uint32_t symbol_size,
+                uint32_t encoded_symbols, uint32_t blocks, uint64_t seed, uint64_t block0)
+        : m_s(std::move(s)), k(symbols), e(encoded_symbols), L(symbol_size), B(blocks),
+          pitch(row_pitch(symbol_size))
+    {
+        // isa.cpp:133-156: erasure choice is part of the (untimed) constructor
+        std::vector<unsigned char> h_err((size_t)B * (e ? e : 1));
+        m_s->check(rsgpu_erasure_patterns(seed, block0, B, (int)k, (int)e, h_err.data()),
+                   "erasure patterns");
+        ws_bytes = rsgpu_decode_workspace_bytes((int)k, (int)e, B);
+        m_s->check(rsgpu_malloc(m_s->ctx, (void**)&err, h_err.size()), "alloc err");
+        m_s->check(rsgpu_malloc(m_s->ctx, (void**)&out, (size_t)B * (e ? e : 1) * pitch), "alloc out");
+        m_s->check(rsgpu_malloc(m_s->ctx, &ws, ws_bytes), "alloc ws");
+        m_s->check(rsgpu_malloc(m_s->ctx, (void**)&status, sizeof(int) * B), "alloc status");
+        m_s->check(rsgpu_malloc(m_s->ctx, (void**)&mism, sizeof(unsigned long long) * B), "alloc");
+        m_s->check(rsgpu_memcpy_h2d(m_s->ctx, err, h_err.data(), h_err.size()), "upload err");
+        h_status.assign(B, -1);
+    }
+    ~gpu_decoder()
+    {
+        rsgpu_free(m_s->ctx, err);
+        rsgpu_free(m_s->ctx, out);
+        rsgpu_free(m_s->ctx, ws);
+        rsgpu_free(m_s->ctx, status);
+        rsgpu_free(m_s->ctx, mism);
+    }
+    // isa.cpp:169-213
+    uint32_t decode_all(const std::shared_ptr<gpu_encoder>& enc)
+    {
+        m_s->check(rsgpu_decode_blocks(m_s->ctx, (int)k, (int)e, L, pitch, B, enc->src, enc->par,
+                                       err, out, ws, status),
+                   "rsgpu_decode_blocks");
+        m_decoded = true;
+        return enc->payload_count();
+    }
+    void finish()
+    {
+        m_s->check(rsgpu_memcpy_d2h(m_s->ctx, h_status.data(), status, sizeof(int) * B), "status");
+    }
+    // isa.cpp:231 (complete iff every block's matrix inverted)
+    bool is_complete() const
+    {
+        if (!m_decoded)
+            return false;
+        for (int st : h_status)
+            if (st != 0)
+                return false;
+        return true;
+    }
+    // isa.cpp:215-229
+    bool verify_data(const std::shared_ptr<gpu_encoder>& enc)
+    {
+        std::vector<unsigned long long> h(B, 0);
+        m_s->check(rsgpu_memcpy_h2d(m_s->ctx, mism, h.data(), sizeof(unsigned long long) * B),
+                   "zero");
+        m_s->check(rsgpu_verify_blocks(m_s->ctx, (int)k, (int)e, L, pitch, B, enc->src, out, err,
+                                       mism),
+                   "verify");
+        m_s->check(rsgpu_memcpy_d2h(m_s->ctx, h.data(), mism, sizeof(unsigned long long) * B),
+                   "mismatch");
+        for (auto v : h)
+            if (v)
+                return false;
+        return true;
+    }
+    uint32_t block_size() const { return k * L; }
+
+    std::shared_ptr<gpu_session> m_s;
+    uint32_t k, e, L, B;
+    size_t pitch, ws_bytes = 0;
+    unsigned char* err = nullptr;
+    unsigned char* out = nullptr;
+    void* ws = nullptr;
+    int* status = nullptr;
+    unsigned long long* mism = nullptr;
+    std::vector<int> h_status;
+    bool m_decoded = false;
+};
+
+}  // namespace sbamd

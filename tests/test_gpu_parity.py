@@ -1,0 +1,242 @@
+"""GPU parity: the HIP path through the C ABI vs the oracle and the reference's
+golden vectors (bit-exact: all work is byte arithmetic).
+
+Small sizes are compared byte-for-byte with the CPU oracle; the benchmark
+sizes (symbol_size 1e6, 16..100 symbols) are checked through the
+size-independent round trip encode -> erase -> decode -> verify on the device,
+plus sampled rows against the oracle.
+"""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+import rsgpu  # noqa: E402
+from oracle_lib import Oracle  # noqa: E402
+from golden.synth import erasure_pattern, synth_block, synth_row  # noqa: E402
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+GOLD = json.load(open(os.path.join(HERE, "golden", "golden.json")))
+
+
+def sha(b):
+    return hashlib.sha256(np.ascontiguousarray(b).tobytes()).hexdigest()
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    assert torch.cuda.is_available(), "GPU test needs a HIP device"
+    c = rsgpu.Context(0)
+    c.set_torch_stream()
+    yield c
+    torch.cuda.synchronize()
+    c.close()
+
+
+@pytest.fixture(scope="module")
+def orc():
+    return Oracle()
+
+
+def dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+def test_fill_synthetic_matches_definition(ctx):
+    for L, pitch in ((1000, 1024), (8191, 8192), (17, 32), (64, 64)):
+        rows = 5
+        buf = torch.zeros(rows * pitch, dtype=torch.uint8, device="cuda")
+        ctx.fill_synthetic(buf, rows, L, pitch, 77, 10)
+        got = buf.view(rows, pitch).cpu().numpy()
+        for r in range(rows):
+            assert (got[r, :L] == synth_row(77, 10 + r, L)).all()
+            assert (got[r, L:] == 0).all()
+
+
+@pytest.mark.parametrize("case", GOLD["cases"], ids=lambda c: f"k{c['k']}e{c['e']}L{c['len']}")
+def test_golden_batched_encode_decode(ctx, case):
+    """Batched encode (specialized or generic) + device decode vs the
+    reference's golden parity hashes and recovered bytes."""
+    k, e, L = case["k"], case["e"], case["len"]
+    B = len(case["blocks"])
+    seed = GOLD["seed"]
+    enc = rsgpu.GpuEncoder(k, L, e, blocks=B, seed=seed, ctx=ctx)
+    enc.encode_all()
+    dec = rsgpu.GpuDecoder(k, L, e, blocks=B, seed=seed, ctx=ctx)
+    assert dec.decode_all(enc) == e
+    torch.cuda.synchronize()
+    assert dec.is_complete()
+    assert dec.verify_data(enc)
+    for b in case["blocks"]:
+        blk = b["blk"]
+        src = enc.source_rows(blk)
+        assert [sha(r) for r in src] == b["src_sha"]
+        par = enc.parity_rows(blk)
+        assert [sha(p) for p in par] == b["parity_sha"], "parity differs from ISA-L"
+        assert dec.err_host[blk].tolist() == b["err"]
+        rec = dec.recovered_rows(blk)
+        for i, s in enumerate(b["err"]):
+            assert (rec[i] == src[s]).all()
+
+
+@pytest.mark.parametrize("k,e,L", [(16, 4, 4096), (64, 32, 4096), (100, 20, 4096), (7, 3, 1024),
+                                   (16, 8, 64000), (33, 31, 2048)])
+def test_generic_encode_equals_specialized_and_oracle(ctx, orc, k, e, L):
+    B = 3
+    enc = rsgpu.GpuEncoder(k, L, e, blocks=B, seed=5, ctx=ctx)
+    enc.encode_all()
+    spec = enc.par.clone()
+    a = rsgpu.gf_gen_rs_matrix(k + e, k)
+    # explicit coefficients force the runtime-coefficient kernel
+    ctx.encode_blocks(k, e, L, enc.pitch, B, enc.src, enc.par, coef=a[k:])
+    torch.cuda.synchronize()
+    assert torch.equal(spec, enc.par)
+    for blk in range(B):
+        data = list(enc.source_rows(blk))
+        ref = orc.encode_block(data, e)
+        got = enc.parity_rows(blk)
+        for p in range(e):
+            assert (got[p] == ref[p]).all()
+
+
+def test_cauchy_encode_golden(ctx):
+    g = GOLD["cauchy_9_5"]
+    ca = np.frombuffer(bytes.fromhex(g["matrix_hex"]), np.uint8).reshape(9, 5)
+    L = g["len"]
+    enc = rsgpu.GpuEncoder(5, L, 4, blocks=1, seed=GOLD["seed"], ctx=ctx, block0=g["blk"])
+    ctx.encode_blocks(5, 4, L, enc.pitch, 1, enc.src, enc.par, coef=ca[5:])
+    par = enc.parity_rows(0)
+    assert [p.tobytes().hex() for p in par] == g["parity_hex"]
+
+
+@pytest.mark.parametrize("length", [0, 1, 15, 16, 17, 33, 100, 4095, 8191, 65537])
+def test_ec_encode_data_pointer_api_any_length(ctx, orc, length):
+    """rsgpu_ec_encode_data == ec_encode_data_base for odd lengths
+    (erasure_code_base_test.c:687-760 sweeps odd lengths)."""
+    rng = np.random.default_rng(length)
+    k, rows = 11, 6
+    coef = rng.integers(0, 256, (rows, k), dtype=np.uint8)
+    g = orc.init_tables(k, rows, coef)
+    data = [rng.integers(0, 256, max(length, 1), dtype=np.uint8) for _ in range(k)]
+    d_data = [dev(d) for d in data]
+    d_out = [torch.zeros(max(length, 1), dtype=torch.uint8, device="cuda") for _ in range(rows)]
+    ctx.ec_encode_data(length, k, rows, g, d_data, d_out)
+    torch.cuda.synchronize()
+    ref = [np.zeros(max(length, 1), np.uint8) for _ in range(rows)]
+    if length:
+        orc.encode_data(length, k, rows, g, data, ref)
+    for r in range(rows):
+        assert (d_out[r].cpu().numpy()[:length] == ref[r][:length]).all()
+
+
+def test_ec_encode_data_misaligned_pointers(ctx, orc):
+    """Random pointer misalignment (erasure_code_base_test.c:566-685)."""
+    rng = np.random.default_rng(9)
+    k, rows, L = 9, 5, 3001
+    coef = rng.integers(0, 256, (rows, k), dtype=np.uint8)
+    g = orc.init_tables(k, rows, coef)
+    data = [rng.integers(0, 256, L, dtype=np.uint8) for _ in range(k)]
+    pool = torch.zeros((k + rows) * (L + 64), dtype=torch.uint8, device="cuda")
+    offs = [int(rng.integers(0, 32)) + i * (L + 64) for i in range(k + rows)]
+    for j in range(k):
+        pool[offs[j]: offs[j] + L] = dev(data[j])
+    base = pool.data_ptr()
+    ctx.ec_encode_data(L, k, rows, g, [base + offs[j] for j in range(k)],
+                       [base + offs[k + r] for r in range(rows)])
+    torch.cuda.synchronize()
+    ref = [np.zeros(L, np.uint8) for _ in range(rows)]
+    orc.encode_data(L, k, rows, g, data, ref)
+    host = pool.cpu().numpy()
+    for r in range(rows):
+        o = offs[k + r]
+        assert (host[o: o + L] == ref[r]).all()
+        # pad bytes after the output untouched
+        assert (host[o + L: o + L + 16] == 0).all()
+
+
+@pytest.mark.parametrize("length", [1, 64, 1000, 4096, 70001])
+def test_ec_encode_data_update(ctx, orc, length):
+    rng = np.random.default_rng(length + 1)
+    k, rows = 8, 5
+    coef = rng.integers(0, 256, (rows, k), dtype=np.uint8)
+    g = orc.init_tables(k, rows, coef)
+    data = rng.integers(0, 256, length, dtype=np.uint8)
+    start = [rng.integers(0, 256, length, dtype=np.uint8) for _ in range(rows)]
+    d_out = [dev(s) for s in start]
+    ctx.ec_encode_data_update(length, k, rows, 3, g, dev(data), d_out)
+    torch.cuda.synchronize()
+    ref = [s.copy() for s in start]
+    orc.encode_data_update(length, k, rows, 3, g, data, ref)
+    for r in range(rows):
+        assert (d_out[r].cpu().numpy() == ref[r]).all()
+
+
+@pytest.mark.parametrize("k,e,L,B", [(16, 4, 1000000, 2), (64, 32, 1000000, 2),
+                                     (100, 20, 1000000, 2), (64, 32, 32000, 64),
+                                     (16, 8, 64000, 8)])
+def test_benchmark_sizes_round_trip(ctx, orc, k, e, L, B):
+    """Configs of BASELINE.json at full symbol size: encode -> erase -> decode ->
+    device verify for every block; block 0's parity rows sampled vs oracle."""
+    seed = 1234
+    enc = rsgpu.GpuEncoder(k, L, e, blocks=B, seed=seed, ctx=ctx)
+    enc.encode_all()
+    dec = rsgpu.GpuDecoder(k, L, e, blocks=B, seed=seed, ctx=ctx)
+    dec.decode_all(enc)
+    torch.cuda.synchronize()
+    assert dec.is_complete()
+    assert dec.verify_data(enc)
+    # sampled bytes vs the oracle on a 4 KiB window of block B-1
+    blk = B - 1
+    src = enc.source_rows(blk)
+    win = slice(L // 2, L // 2 + 4096) if L >= 8192 else slice(0, L)
+    data = [np.ascontiguousarray(s[win]) for s in src]
+    ref = orc.encode_block(data, e)
+    par = enc.parity_rows(blk)
+    for p in range(e):
+        assert (par[p][win] == ref[p]).all()
+    # the erasures are the ones the definition picks
+    assert dec.err_host[blk].tolist() == erasure_pattern(seed, blk, k, e).tolist()
+
+
+def test_decode_matches_oracle_decode_rows(ctx, orc):
+    """Decoding also recovers from a parity buffer that was produced by the
+    oracle (cross-implementation), and recovers garbage-free bytes."""
+    k, e, L, B = 20, 7, 2048, 3
+    enc = rsgpu.GpuEncoder(k, L, e, blocks=B, seed=8, ctx=ctx)
+    pv = enc.par.view(B, e, enc.pitch)
+    for blk in range(B):
+        data = list(synth_block(8, blk, k, L))
+        ref = orc.encode_block(data, e)
+        for p in range(e):
+            pv[blk, p, :L] = dev(ref[p])
+    dec = rsgpu.GpuDecoder(k, L, e, blocks=B, seed=8, ctx=ctx)
+    dec.decode_all(enc)
+    torch.cuda.synchronize()
+    assert dec.is_complete() and dec.verify_data(enc)
+
+
+def test_all_erasure_counts_small(ctx):
+    """Every erasure count 1..k for small k (edge: e == k, only parity left)."""
+    k, L = 12, 512
+    for e in range(1, k + 1):
+        enc = rsgpu.GpuEncoder(k, L, e, blocks=2, seed=e, ctx=ctx)
+        enc.encode_all()
+        dec = rsgpu.GpuDecoder(k, L, e, blocks=2, seed=e, ctx=ctx)
+        dec.decode_all(enc)
+        torch.cuda.synchronize()
+        assert dec.is_complete() and dec.verify_data(enc), e
+
+
+def test_throughput_benchmark_mirror(ctx):
+    tb = rsgpu.ThroughputBenchmark(symbols=(16,), loss_rate=(0.5,), symbol_size=(64000,),
+                                   blocks=4, ctx=ctx)
+    cfgs = tb.configurations()
+    assert [c.type for c in cfgs] == ["encoder", "decoder"]
+    for c in cfgs:
+        row = tb.run(c)
+        assert row["accepted"] and row["goodput"] > 0
