@@ -116,7 +116,7 @@ size_t rsgpu_decode_workspace_bytes(int k, int e, size_t blocks);
  * originals and all e parity rows.  On the device: survivor matrix ->
  * gf_invert_matrix -> decode rows -> dot product into out[b][i] (symbol
  * d_err[b][i]).  d_status[b] = 0, or -1 for a singular matrix ("BAD MATRIX",
- * isa.cpp:185-190; that block's output is untouched).  d_workspace holds
+ * isa.cpp:185-190; that block's output is unspecified).  d_workspace holds
  * rsgpu_decode_workspace_bytes() bytes. */
 int rsgpu_decode_blocks(rsgpu_ctx *ctx, int k, int e, size_t len, size_t pitch, size_t blocks,
                         const unsigned char *d_src, const unsigned char *d_parity,

@@ -1,0 +1,398 @@
+// rs_bitsliced.hip -- bit-sliced RS(K, E) parity / syndrome kernel with
+// compile-time coefficients (the gf_gen_rs_matrix code, isa/ec_base.c:62-79).
+//
+// Why bit-slicing: on gfx950 a wave64 v_bitop3/v_xor/v_and issues in ~2
+// cycles per SIMD but v_perm/v_pk_*/v_bfi in ~4 (profiles/r1_ubench_valu.log),
+// and the GF(2^8) product by a constant is GF(2)-linear.  With each lane
+// holding 32 consecutive bytes of a row as 8 bit-planes (plane a = bit a of
+// the 32 bytes), multiplying by a constant c and accumulating is, per output
+// plane, one 3-input XOR of two "four Russians" entries
+//     out_b ^= L[m_b & 15] ^ H[m_b >> 4],
+// L[n] = XOR of planes 0..3 selected by n, H[n] = same for planes 4..7, m_b =
+// row b of c's 8x8 bit matrix.  That is 8 full-rate ops per (coefficient,
+// 32 bytes) versus 24 quarter-rate v_perm for the same bytes.
+//
+// Code size: the parity matrix has entries 2^(r*j).  Sources are processed in
+// chunks of C with Horner's rule over chunks,
+//     p_r = sum_c 2^(C r c) * E_c(r),   E_c(r) = sum_t 2^(r t) d_{cC+t},
+// so one chunk's straight-line code (coefficients 2^(r t), t < C) serves
+// every chunk; between chunks each accumulator is multiplied by the constant
+// 2^(C r) (~16 XORs).  The chunk loop is a runtime loop.
+//
+// Work split: a workgroup of NW waves shares 64 x 32 = 2048 byte positions;
+// wave w owns outputs [w*OPW, (w+1)*OPW) (8 planes x OPW accumulators in
+// VGPRs, <= 128 VGPRs for 4 waves/SIMD).  The NW waves divide each chunk's
+// sources for loading + transposing into LDS, then all read every source's
+// planes from LDS.  Bit transposes are SWAR 8x8 bit-matrix transposes across
+// the lane's 8 dwords (12 block swaps), and the same routine converts the
+// accumulators back to bytes.
+//
+// SYN (decode): sources whose bit is set in the block's erasure mask are
+// skipped and the finished sums are XORed with the parity rows, giving the
+// syndromes s_p = P_p ^ sum_{j not erased} 2^(p j) d_j.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <utility>
+
+#include "gf256.h"
+#include "rs_kernels.h"
+
+namespace rsgpu {
+namespace bs {
+
+// row b of the 8x8 GF(2) matrix of "multiply by c": bit a set iff bit b of
+// c * 2^a is set (column a = c * 2^a, computed by doubling)
+constexpr uint8_t mat_row(uint8_t c, int b)
+{
+    uint8_t row = 0;
+    uint8_t v = c;
+    for (int a = 0; a < 8; ++a) {
+        if ((v >> b) & 1)
+            row |= (uint8_t)(1u << a);
+        v = (uint8_t)((v << 1) ^ ((v & 0x80) ? 0x1D : 0));
+    }
+    return row;
+}
+
+template <int K, int E, int C>
+struct Plan {
+    uint8_t inner[E][C][8];  // rows of 2^(r t)
+    uint8_t tw[E][8];        // rows of 2^(C r)
+    constexpr Plan() : inner(), tw()
+    {
+        uint8_t g = 1;  // 2^r
+        for (int r = 0; r < E; ++r) {
+            uint8_t v = 1;  // 2^(r t)
+            for (int t = 0; t < C; ++t) {
+                for (int b = 0; b < 8; ++b)
+                    inner[r][t][b] = mat_row(v, b);
+                v = gf_mul_slow(v, g);
+            }
+            // v == 2^(r C) now
+            for (int b = 0; b < 8; ++b)
+                tw[r][b] = mat_row(v, b);
+            g = gf_mul_slow(g, 2);
+        }
+    }
+};
+
+template <int K, int E, int C>
+struct PlanHolder {
+    static constexpr Plan<K, E, C> p{};
+};
+
+__device__ __forceinline__ uint32_t x3(uint32_t a, uint32_t b, uint32_t c)
+{
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+
+// Opaque VGPR copy of a constant: keeps masks out of SGPR operands (an SGPR
+// operand makes v_bitop3 a 4-cycle issue, profiles/r1_ubench_valu.log).
+__device__ __forceinline__ uint32_t vconst(uint32_t c)
+{
+    uint32_t v;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(v) : "i"(c));
+    return v;
+}
+
+// (lo, hi) block swap of the SWAR 8x8 bit transpose, per byte lane:
+//   lo' = (lo & m) | ((hi << s) & ~m),  hi' = ((lo >> s) & m) | (hi & ~m)
+// bitop3 truth tables (src0=0xF0, src1=0xCC, src2=0xAA):
+//   f(a, b, m) = (a & m) | (b & ~m)  -> (0xF0 & 0xAA) | (0xCC & 0x55) = 0xE4
+template <int S>
+__device__ __forceinline__ void swap_blk(uint32_t& lo, uint32_t& hi, uint32_t m)
+{
+    const uint32_t hs = hi << S;
+    const uint32_t ls = lo >> S;
+    const uint32_t nl = __builtin_amdgcn_bitop3_b32(lo, hs, m, 0xE4);
+    const uint32_t nh = __builtin_amdgcn_bitop3_b32(ls, hi, m, 0xE4);
+    lo = nl;
+    hi = nh;
+}
+
+// In place: W[w] byte q = byte (4w+q) of a 32-byte segment  <->  plane
+// layout W[a] byte q bit w = bit a of that byte.  Self-inverse.
+__device__ __forceinline__ void tr8(uint32_t (&W)[8], uint32_t m4, uint32_t m2, uint32_t m1)
+{
+    swap_blk<4>(W[0], W[4], m4);
+    swap_blk<4>(W[1], W[5], m4);
+    swap_blk<4>(W[2], W[6], m4);
+    swap_blk<4>(W[3], W[7], m4);
+    swap_blk<2>(W[0], W[2], m2);
+    swap_blk<2>(W[1], W[3], m2);
+    swap_blk<2>(W[4], W[6], m2);
+    swap_blk<2>(W[5], W[7], m2);
+    swap_blk<1>(W[0], W[1], m1);
+    swap_blk<1>(W[2], W[3], m1);
+    swap_blk<1>(W[4], W[5], m1);
+    swap_blk<1>(W[6], W[7], m1);
+}
+
+// acc ^= L[M & 15] ^ H[M >> 4] with zero entries elided at compile time
+template <int M>
+__device__ __forceinline__ void fold(uint32_t& acc, const uint32_t (&Lt)[16], const uint32_t (&Ht)[16])
+{
+    constexpr int lo = M & 15, hi = M >> 4;
+    if constexpr (lo != 0 && hi != 0)
+        acc = x3(acc, Lt[lo], Ht[hi]);
+    else if constexpr (lo != 0)
+        acc ^= Lt[lo];
+    else if constexpr (hi != 0)
+        acc ^= Ht[hi];
+}
+
+template <class P, int R, int T, int... Bs>
+__device__ __forceinline__ void fold_row(uint32_t (&acc)[8], const uint32_t (&Lt)[16],
+                                         const uint32_t (&Ht)[16], std::integer_sequence<int, Bs...>)
+{
+    (fold<P::p.inner[R][T][Bs]>(acc[Bs], Lt, Ht), ...);
+}
+
+template <class P, int R0, int T, int NR, int... Rs>
+__device__ __forceinline__ void fold_rows(uint32_t (&acc)[NR][8], const uint32_t (&Lt)[16],
+                                          const uint32_t (&Ht)[16], std::integer_sequence<int, Rs...>)
+{
+    (fold_row<P, R0 + Rs, T>(acc[Rs], Lt, Ht, std::make_integer_sequence<int, 8>{}), ...);
+}
+
+// XOR of the planes selected by the constant mask MASK (row of a matrix)
+template <int MASK>
+__device__ __forceinline__ uint32_t xsel(const uint32_t (&v)[8])
+{
+    uint32_t t[8];
+    int n = 0;
+#pragma unroll
+    for (int a = 0; a < 8; ++a)
+        if ((MASK >> a) & 1)
+            t[n++] = v[a];
+    if (n == 0)
+        return 0;
+    uint32_t s = t[0];
+    int i = 1;
+    while (i + 1 < n) {
+        s = x3(s, t[i], t[i + 1]);
+        i += 2;
+    }
+    if (i < n)
+        s ^= t[i];
+    return s;
+}
+
+template <class P, int R, int... Bs>
+__device__ __forceinline__ void twiddle_row(uint32_t (&acc)[8], std::integer_sequence<int, Bs...>)
+{
+    uint32_t o[8] = {xsel<P::p.tw[R][Bs]>(acc)...};
+#pragma unroll
+    for (int b = 0; b < 8; ++b)
+        acc[b] = o[b];
+}
+
+template <class P, int R0, int NR, int... Rs>
+__device__ __forceinline__ void twiddle_rows(uint32_t (&acc)[NR][8], std::integer_sequence<int, Rs...>)
+{
+    (twiddle_row<P, R0 + Rs>(acc[Rs], std::make_integer_sequence<int, 8>{}), ...);
+}
+
+__device__ __forceinline__ void build_lh(const uint32_t (&p)[8], uint32_t (&Lt)[16], uint32_t (&Ht)[16])
+{
+    Lt[0] = 0;
+    Ht[0] = 0;
+#pragma unroll
+    for (int n = 1; n < 16; ++n) {
+        const int low = n & -n;
+        const int bit = low == 1 ? 0 : low == 2 ? 1 : low == 4 ? 2 : 3;
+        Lt[n] = (n == low) ? p[bit] : (Lt[n ^ low] ^ p[bit]);
+        Ht[n] = (n == low) ? p[4 + bit] : (Ht[n ^ low] ^ p[4 + bit]);
+    }
+}
+
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) const v4u gcv4u;
+typedef __attribute__((address_space(1))) v4u gv4u;
+
+__device__ __forceinline__ void load32(const uint8_t* row, long long off, bool ok, uint32_t (&W)[8])
+{
+    if (ok) {
+        const v4u a = *(gcv4u*)(row + off);
+        const v4u b = *(gcv4u*)(row + off + 16);
+        W[0] = a.x; W[1] = a.y; W[2] = a.z; W[3] = a.w;
+        W[4] = b.x; W[5] = b.y; W[6] = b.z; W[7] = b.w;
+    } else {
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+            W[i] = 0;
+    }
+}
+
+__device__ __forceinline__ void store32(uint8_t* row, long long off, const uint32_t (&W)[8])
+{
+    v4u a, b;
+    a.x = W[0]; a.y = W[1]; a.z = W[2]; a.w = W[3];
+    b.x = W[4]; b.y = W[5]; b.z = W[6]; b.w = W[7];
+    *(gv4u*)(row + off) = a;
+    *(gv4u*)(row + off + 16) = b;
+}
+
+// consume source T of the chunk from planes p (all lanes), for this wave's rows
+template <class P, int R0, int NR, int T>
+__device__ __forceinline__ void consume(uint32_t (&acc)[NR][8], const uint32_t (&p)[8])
+{
+    uint32_t Lt[16], Ht[16];
+    build_lh(p, Lt, Ht);
+    fold_rows<P, R0, T, NR>(acc, Lt, Ht, std::make_integer_sequence<int, NR>{});
+}
+
+struct Args {
+    const uint8_t* src;   // [B][K] rows
+    const uint8_t* par;   // [B][E] parity rows (SYN only)
+    uint8_t* out;         // [B][E] rows
+    long long pitch, len;
+    const uint64_t* emask;  // [B][2] erasure bitmask of the K originals (SYN only)
+};
+
+// One wave group: rows [R0, R0+NR).  LDS ring: [C][2][64] uint4 per chunk.
+template <int K, int E, int C, int NW, bool SYN, int G>
+__device__ __forceinline__ void run_group(const Args& a, uint4* lds)
+{
+    using P = PlanHolder<K, E, C>;
+    constexpr int OPW = (E + NW - 1) / NW;
+    constexpr int R0 = G * OPW;
+    constexpr int NR = (E - R0) < OPW ? (E - R0) : OPW;
+    constexpr int NCH = (K + C - 1) / C;
+    static_assert(NR > 0, "empty wave group");
+
+    const int lane = threadIdx.x & 63;
+    const int b = blockIdx.y;
+    const long long off = (long long)blockIdx.x * 2048 + lane * 32;
+    const bool inb = off + 32 <= a.len;
+    const uint8_t* sb = a.src + (size_t)b * K * a.pitch;
+    uint64_t em0 = 0, em1 = 0;
+    if constexpr (SYN) {
+        em0 = a.emask[2 * b];
+        em1 = a.emask[2 * b + 1];
+    }
+    const uint32_t m4 = vconst(0x0F0F0F0Fu), m2 = vconst(0x33333333u), m1 = vconst(0x55555555u);
+
+    uint32_t acc[NR][8];
+#pragma unroll
+    for (int r = 0; r < NR; ++r)
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+            acc[r][q] = 0;
+
+    for (int ch = NCH - 1; ch >= 0; --ch) {
+        if constexpr (NW > 1) {
+            // load + transpose this wave's share of the chunk into LDS
+#pragma unroll
+            for (int t = G; t < C; t += NW) {
+                const int j = ch * C + t;
+                bool live = j < K;
+                if constexpr (SYN)
+                    live = live && !(((j < 64 ? em0 >> j : em1 >> (j - 64)) & 1));
+                uint32_t W[8];
+                load32(sb + (size_t)j * a.pitch, off, live && inb, W);
+                tr8(W, m4, m2, m1);
+                lds[(t * 2 + 0) * 64 + lane] = make_uint4(W[0], W[1], W[2], W[3]);
+                lds[(t * 2 + 1) * 64 + lane] = make_uint4(W[4], W[5], W[6], W[7]);
+            }
+            __syncthreads();
+        }
+        if (ch != NCH - 1)
+            twiddle_rows<P, R0, NR>(acc, std::make_integer_sequence<int, NR>{});
+        [&]<int... Ts>(std::integer_sequence<int, Ts...>) {
+            (
+                [&] {
+                    constexpr int T = Ts;
+                    const int j = ch * C + T;
+                    bool live = j < K;
+                    if constexpr (SYN)
+                        live = live && !(((j < 64 ? em0 >> j : em1 >> (j - 64)) & 1));
+                    if (live) {
+                        uint32_t p[8];
+                        if constexpr (NW > 1) {
+                            const uint4 u = lds[(T * 2 + 0) * 64 + lane];
+                            const uint4 v = lds[(T * 2 + 1) * 64 + lane];
+                            p[0] = u.x; p[1] = u.y; p[2] = u.z; p[3] = u.w;
+                            p[4] = v.x; p[5] = v.y; p[6] = v.z; p[7] = v.w;
+                        } else {
+                            load32(sb + (size_t)j * a.pitch, off, inb, p);
+                            tr8(p, m4, m2, m1);
+                        }
+                        consume<P, R0, NR, T>(acc, p);
+                    }
+                }(),
+                ...);
+        }(std::make_integer_sequence<int, C>{});
+        if constexpr (NW > 1)
+            __syncthreads();
+    }
+
+    if (!inb)
+        return;
+    uint8_t* ob = a.out + (size_t)b * E * a.pitch;
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+        uint32_t W[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+            W[q] = acc[r][q];
+        tr8(W, m4, m2, m1);
+        if constexpr (SYN) {
+            uint32_t Pp[8];
+            load32(a.par + ((size_t)b * E + R0 + r) * a.pitch, off, true, Pp);
+#pragma unroll
+            for (int q = 0; q < 8; ++q)
+                W[q] ^= Pp[q];
+        }
+        store32(ob + (size_t)(R0 + r) * a.pitch, off, W);
+    }
+}
+
+template <int K, int E, int C, int NW, bool SYN>
+__global__ __launch_bounds__(64 * NW, 4) void k_rs_bs(Args a)
+{
+    __shared__ uint4 lds[NW > 1 ? C * 2 * 64 : 1];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    [&]<int... Gs>(std::integer_sequence<int, Gs...>) {
+        ((wave == Gs ? run_group<K, E, C, NW, SYN, Gs>(a, lds) : void()), ...);
+    }(std::make_integer_sequence<int, NW>{});
+}
+
+template <int K, int E, int C, int NW>
+hipError_t launch(const uint8_t* src, const uint8_t* par, uint8_t* out, long long pitch,
+                  long long len, long long blocks, const uint64_t* emask, hipStream_t st)
+{
+    Args a{src, par, out, pitch, len, emask};
+    dim3 grid((unsigned)((len + 2047) / 2048), (unsigned)blocks);
+    if (emask)
+        hipLaunchKernelGGL((k_rs_bs<K, E, C, NW, true>), grid, dim3(64 * NW), 0, st, a);
+    else
+        hipLaunchKernelGGL((k_rs_bs<K, E, C, NW, false>), grid, dim3(64 * NW), 0, st, a);
+    return hipGetLastError();
+}
+
+}  // namespace bs
+
+bool rs_bitsliced_available(int k, int e)
+{
+    return (k == 16 && e == 4) || (k == 16 && e == 8) || (k == 64 && e == 32) ||
+           (k == 100 && e == 20) || (k == 5 && e == 4) || (k == 20 && e == 7) ||
+           (k == 64 && e == 16);
+}
+
+hipError_t launch_rs_bitsliced(int k, int e, const uint8_t* src, const uint8_t* par, uint8_t* out,
+                               long long pitch, long long len, long long blocks,
+                               const uint64_t* emask, hipStream_t st)
+{
+    if (k == 16 && e == 4) return bs::launch<16, 4, 16, 1>(src, par, out, pitch, len, blocks, emask, st);
+    if (k == 16 && e == 8) return bs::launch<16, 8, 16, 1>(src, par, out, pitch, len, blocks, emask, st);
+    if (k == 64 && e == 32) return bs::launch<64, 32, 16, 4>(src, par, out, pitch, len, blocks, emask, st);
+    if (k == 64 && e == 16) return bs::launch<64, 16, 16, 2>(src, par, out, pitch, len, blocks, emask, st);
+    if (k == 100 && e == 20) return bs::launch<100, 20, 20, 4>(src, par, out, pitch, len, blocks, emask, st);
+    if (k == 5 && e == 4) return bs::launch<5, 4, 5, 1>(src, par, out, pitch, len, blocks, emask, st);
+    if (k == 20 && e == 7) return bs::launch<20, 7, 20, 1>(src, par, out, pitch, len, blocks, emask, st);
+    return hipErrorInvalidValue;
+}
+
+}  // namespace rsgpu

@@ -44,6 +44,22 @@ hipError_t launch_fill_synth(uint8_t* dst, long long rows, long long len, long l
 hipError_t launch_compare_rows(const uint8_t* src, long long src_pitch, int k, const uint8_t* out,
                                long long out_pitch, int e, const uint8_t* err, long long len,
                                long long blocks, unsigned long long* mismatches, hipStream_t st);
+// Bit-sliced RS(k, e) with compile-time coefficients (rs_bitsliced.hip).
+// emask == nullptr: parity of the gf_gen_rs_matrix code into `out`.
+// emask != nullptr ([blocks][2] bitmask of erased originals): syndromes
+//   out[p] = par[p] ^ sum_{j not erased} 2^(p j) src[j].
+// Requires len % 32 == 0, 16-byte aligned rows.
+bool rs_bitsliced_available(int k, int e);
+hipError_t launch_rs_bitsliced(int k, int e, const uint8_t* src, const uint8_t* par, uint8_t* out,
+                               long long pitch, long long len, long long blocks,
+                               const uint64_t* emask, hipStream_t st);
+
+hipError_t launch_decode_prepare_syn(int k, int e, int rows_pad, long long blocks,
+                                     const uint8_t* err, uint8_t* out, long long out_pitch,
+                                     const uint8_t** srcs, uint8_t** dsts, uint4* tabs4,
+                                     uint32_t* ctab, long long tab_block_stride,
+                                     unsigned long long* emask, int* status, hipStream_t st);
+
 hipError_t launch_row_ptrs(const uint8_t* base, long long pitch, int rows_per_block,
                            long long blocks, const uint8_t** out, hipStream_t st);
 hipError_t launch_update(const uint8_t* data, uint8_t* const* coding, const uint4* tabs4,

@@ -56,6 +56,20 @@ __device__ __forceinline__ uint4 gload16(const uint8_t* p, long long w)
     const u32x4 v = ((g_cu32x4*)p)[w];
     return make_uint4(v.x, v.y, v.z, v.w);
 }
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(1))) const u32x2 g_cu32x2;
+typedef __attribute__((address_space(1))) u32x2 g_u32x2;
+__device__ __forceinline__ uint2 gload8(const uint8_t* p, long long w)
+{
+    const u32x2 v = ((g_cu32x2*)p)[w];
+    return make_uint2(v.x, v.y);
+}
+__device__ __forceinline__ void gstore8(uint8_t* p, long long w, uint2 v)
+{
+    u32x2 t;
+    t.x = v.x; t.y = v.y;
+    ((g_u32x2*)p)[w] = t;
+}
 __device__ __forceinline__ void gstore16(uint8_t* p, long long w, uint4 v)
 {
     u32x4 t;
@@ -85,7 +99,7 @@ __global__ __launch_bounds__(256) void k_dot_generic(const uint8_t* const* __res
                                                      const uint4* __restrict__ tabs4,
                                                      const uint32_t* __restrict__ ctab,
                                                      long long tab_block_stride, int k, int rows,
-                                                     int rows_pad, int row0, long long n_ow,
+                                                     int rows_pad, int row0, long long n_qw,
                                                      const int* __restrict__ status)
 {
     extern __shared__ uint4 ltab[];  // [k][R]
@@ -104,37 +118,63 @@ __global__ __launch_bounds__(256) void k_dot_generic(const uint8_t* const* __res
     }
     __syncthreads();
 
-    for (long long w = (long long)blockIdx.x * blockDim.x + threadIdx.x; w < n_ow;
+    for (long long w = (long long)blockIdx.x * blockDim.x + threadIdx.x; w < n_qw;
          w += (long long)gridDim.x * blockDim.x) {
-        uint4 acc[R];
+        uint32_t acc0[R], acc1[R];
 #pragma unroll
-        for (int r = 0; r < R; ++r)
-            acc[r] = make_uint4(0, 0, 0, 0);
-        uint4 xn = gload16(S[0], w);
-        for (int j = 0; j < k; ++j) {
-            const uint4 x = xn;
-            if (j + 1 < k)
-                xn = gload16(S[j + 1], w);
-            const uint32_t s0x = x.x & 0x07070707u, s1x = (x.x >> 3) & 0x07070707u, s2x = (x.x >> 6) & 0x03030303u;
-            const uint32_t s0y = x.y & 0x07070707u, s1y = (x.y >> 3) & 0x07070707u, s2y = (x.y >> 6) & 0x03030303u;
-            const uint32_t s0z = x.z & 0x07070707u, s1z = (x.z >> 3) & 0x07070707u, s2z = (x.z >> 6) & 0x03030303u;
-            const uint32_t s0w = x.w & 0x07070707u, s1w = (x.w >> 3) & 0x07070707u, s2w = (x.w >> 6) & 0x03030303u;
-            const uint4* lt = ltab + j * R;
-            const uint32_t* ct = TC + (size_t)j * rows_pad;
+        for (int r = 0; r < R; ++r) {
+            acc0[r] = 0;
+            acc1[r] = 0;
+        }
+        // two sources per step: the six lookups of a (row, dword) pair fold
+        // into the accumulator with three 3-input XORs
+        uint2 xa = gload8(S[0], w);
+        uint2 xb = k > 1 ? gload8(S[1], w) : make_uint2(0, 0);
+        int j = 0;
+        for (; j + 1 < k; j += 2) {
+            const uint2 a = xa, bb = xb;
+            if (j + 2 < k)
+                xa = gload8(S[j + 2], w);
+            if (j + 3 < k)
+                xb = gload8(S[j + 3], w);
+            const uint32_t a00 = a.x & 0x07070707u, a01 = (a.x >> 3) & 0x07070707u, a02 = (a.x >> 6) & 0x03030303u;
+            const uint32_t a10 = a.y & 0x07070707u, a11 = (a.y >> 3) & 0x07070707u, a12 = (a.y >> 6) & 0x03030303u;
+            const uint32_t b00 = bb.x & 0x07070707u, b01 = (bb.x >> 3) & 0x07070707u, b02 = (bb.x >> 6) & 0x03030303u;
+            const uint32_t b10 = bb.y & 0x07070707u, b11 = (bb.y >> 3) & 0x07070707u, b12 = (bb.y >> 6) & 0x03030303u;
+            const uint4* lta = ltab + j * R;
+            const uint4* ltb = lta + R;
+            const uint32_t* cta = TC + (size_t)j * rows_pad;
+            const uint32_t* ctb = cta + rows_pad;
 #pragma unroll
             for (int r = 0; r < R; ++r) {
-                const uint4 t = lt[r];
-                const uint32_t c = ct[r];
-                acc[r].x = xor3(acc[r].x, vperm(t.y, t.x, s0x), vperm(t.w, t.z, s1x)) ^ vperm(c, c, s2x);
-                acc[r].y = xor3(acc[r].y, vperm(t.y, t.x, s0y), vperm(t.w, t.z, s1y)) ^ vperm(c, c, s2y);
-                acc[r].z = xor3(acc[r].z, vperm(t.y, t.x, s0z), vperm(t.w, t.z, s1z)) ^ vperm(c, c, s2z);
-                acc[r].w = xor3(acc[r].w, vperm(t.y, t.x, s0w), vperm(t.w, t.z, s1w)) ^ vperm(c, c, s2w);
+                const uint4 ta = lta[r], tb = ltb[r];
+                const uint32_t ca = cta[r], cb = ctb[r];
+                acc0[r] = xor3(acc0[r], vperm(ta.y, ta.x, a00), vperm(ta.w, ta.z, a01));
+                acc0[r] = xor3(acc0[r], vperm(ca, ca, a02), vperm(tb.y, tb.x, b00));
+                acc0[r] = xor3(acc0[r], vperm(tb.w, tb.z, b01), vperm(cb, cb, b02));
+                acc1[r] = xor3(acc1[r], vperm(ta.y, ta.x, a10), vperm(ta.w, ta.z, a11));
+                acc1[r] = xor3(acc1[r], vperm(ca, ca, a12), vperm(tb.y, tb.x, b10));
+                acc1[r] = xor3(acc1[r], vperm(tb.w, tb.z, b11), vperm(cb, cb, b12));
+            }
+        }
+        if (j < k) {
+            const uint2 a = xa;
+            const uint32_t a00 = a.x & 0x07070707u, a01 = (a.x >> 3) & 0x07070707u, a02 = (a.x >> 6) & 0x03030303u;
+            const uint32_t a10 = a.y & 0x07070707u, a11 = (a.y >> 3) & 0x07070707u, a12 = (a.y >> 6) & 0x03030303u;
+            const uint4* lta = ltab + j * R;
+            const uint32_t* cta = TC + (size_t)j * rows_pad;
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const uint4 ta = lta[r];
+                const uint32_t ca = cta[r];
+                acc0[r] = xor3(acc0[r], vperm(ta.y, ta.x, a00), vperm(ta.w, ta.z, a01)) ^ vperm(ca, ca, a02);
+                acc1[r] = xor3(acc1[r], vperm(ta.y, ta.x, a10), vperm(ta.w, ta.z, a11)) ^ vperm(ca, ca, a12);
             }
         }
 #pragma unroll
         for (int r = 0; r < R; ++r)
             if (r < nr)
-                gstore16(Dst[row0 + r], w, acc[r]);
+                gstore8(Dst[row0 + r], w, make_uint2(acc0[r], acc1[r]));
     }
 }
 
@@ -549,7 +589,7 @@ __global__ __launch_bounds__(256) void k_compare_rows(const uint8_t* __restrict_
 template <int R>
 static hipError_t launch_generic_R(const DotArgs& a, hipStream_t st)
 {
-    const long long n_ow = a.len / 16;
+    const long long n_ow = a.len / 8;  // 8-byte words per lane
     if (n_ow > 0) {
         const size_t lds = (size_t)a.k * R * sizeof(uint4);
         static bool attr_set = false;
@@ -570,7 +610,7 @@ static hipError_t launch_generic_R(const DotArgs& a, hipStream_t st)
                                a.status);
         }
     }
-    const long long first = n_ow * 16;
+    const long long first = n_ow * 8;
     if (first < a.len) {
         const long long nb = a.len - first;
         dim3 grid((unsigned)((nb + 255) / 256), (unsigned)a.blocks);
@@ -758,6 +798,193 @@ hipError_t launch_update(const uint8_t* data, uint8_t* const* coding, const uint
         g = 1;
     hipLaunchKernelGGL(k_update, dim3((unsigned)g, (unsigned)rows), dim3(256), 0, st, data,
                        coding, tabs4, ctab, len);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Decode preparation, syndrome form (one workgroup per block)
+// ---------------------------------------------------------------------------
+// With all e parity rows surviving and e erased ORIGINALS E = {j_0 < ... },
+// the survivor matrix b of isa.cpp:177-182 is singular iff the e x e block
+// V_E[p][i] = 2^(p*j_i) is (det b = det V_E up to row order).  The recovered
+// symbols are the unique solution of V_E x = s with the syndromes
+// s_p = P_p ^ sum_{j not in E} 2^(p j) d_j, so the decode needs V_E^-1 only.
+// Outputs: emask[b][2], srcs[b][e] = dsts[b][e] = out rows (the syndrome
+// kernel writes s into out; the dot product then runs in place), tables of
+// V_E^-1 as [p][rows_pad], status.
+__global__ __launch_bounds__(256) void k_decode_prepare_syn(int k, int e, int rows_pad,
+                                                            const uint8_t* __restrict__ err,
+                                                            uint8_t* out, long long out_pitch,
+                                                            const uint8_t** srcs, uint8_t** dsts,
+                                                            uint4* tabs4, uint32_t* ctab,
+                                                            long long tab_block_stride,
+                                                            unsigned long long* emask, int* status)
+{
+    extern __shared__ __align__(16) uint8_t lds[];
+    uint8_t* gexp = lds;          // 512
+    uint8_t* glog = lds + 512;    // 256
+    int* sh = reinterpret_cast<int*>(lds + 768);  // 16 ints
+    uint8_t* A = lds + 832;       // e*e
+    uint8_t* Dm = A + e * e;      // e*e
+    const int b = blockIdx.x;
+    const int tid = threadIdx.x, nt = blockDim.x;
+    const uint8_t* eb = err + (size_t)b * e;
+    if (tid == 0) {
+        unsigned v = 1;
+        for (int i = 0; i < 255; ++i) {
+            gexp[i] = (uint8_t)v;
+            gexp[i + 255] = (uint8_t)v;
+            glog[v] = (uint8_t)i;
+            v <<= 1;
+            if (v & 0x100)
+                v ^= 0x11D;
+        }
+        gexp[510] = gexp[0];
+        gexp[511] = gexp[1];
+        glog[0] = 0;
+        // validate: strictly ascending originals
+        int bad = 0;
+        unsigned long long m0 = 0, m1 = 0;
+        for (int i = 0; i < e; ++i) {
+            const int j = eb[i];
+            if (j >= k || (i > 0 && j <= eb[i - 1]))
+                bad = 1;
+            else if (j < 64)
+                m0 |= 1ull << j;
+            else
+                m1 |= 1ull << (j - 64);
+        }
+        emask[2 * b] = m0;
+        emask[2 * b + 1] = m1;
+        sh[0] = bad ? -2 : 0;
+    }
+    __syncthreads();
+    if (sh[0] != 0) {
+        if (tid == 0)
+            status[b] = sh[0];
+        return;
+    }
+    for (int idx = tid; idx < e * e; idx += nt) {
+        const int p = idx / e, i = idx - p * e;
+        A[idx] = gexp[(p * (int)eb[i]) % 255];
+        Dm[idx] = (p == i) ? 1 : 0;
+    }
+    __syncthreads();
+    auto gmul = [&](uint8_t x, uint8_t y) -> uint8_t {
+        return (x && y) ? gexp[glog[x] + glog[y]] : (uint8_t)0;
+    };
+    const int n = e;
+    for (int i = 0; i < n; ++i) {
+        if (tid == 0) {
+            int piv = i;
+            if (A[i * n + i] == 0) {
+                piv = -1;
+                for (int j = i + 1; j < n; ++j)
+                    if (A[j * n + i]) {
+                        piv = j;
+                        break;
+                    }
+            }
+            sh[1] = piv;
+        }
+        __syncthreads();
+        const int piv = sh[1];
+        if (piv < 0) {
+            if (tid == 0)
+                sh[0] = -1;
+            break;
+        }
+        if (piv != i) {
+            for (int c = tid; c < n; c += nt) {
+                uint8_t t = A[i * n + c];
+                A[i * n + c] = A[piv * n + c];
+                A[piv * n + c] = t;
+                t = Dm[i * n + c];
+                Dm[i * n + c] = Dm[piv * n + c];
+                Dm[piv * n + c] = t;
+            }
+            __syncthreads();
+        }
+        const uint8_t pinv = gexp[255 - glog[A[i * n + i]]];
+        __syncthreads();
+        for (int c = tid; c < n; c += nt) {
+            A[i * n + c] = gmul(A[i * n + c], pinv);
+            Dm[i * n + c] = gmul(Dm[i * n + c], pinv);
+        }
+        __syncthreads();
+        for (int idx = tid; idx < n * n; idx += nt) {
+            const int r = idx / n, c = idx - r * n;
+            if (r == i || c == i)
+                continue;
+            const uint8_t f = A[r * n + i];
+            A[idx] ^= gmul(f, A[i * n + c]);
+            Dm[idx] ^= gmul(f, Dm[i * n + c]);
+        }
+        __syncthreads();
+        for (int r = tid; r < n; r += nt) {
+            if (r == i)
+                continue;
+            const uint8_t f = A[r * n + i];
+            Dm[r * n + i] ^= gmul(f, Dm[i * n + i]);
+            A[r * n + i] = 0;
+        }
+        __syncthreads();
+    }
+    __syncthreads();
+    const int st = sh[0];
+    if (tid == 0)
+        status[b] = st;
+    for (int i = tid; i < e; i += nt) {
+        uint8_t* row = out + ((size_t)b * e + i) * out_pitch;
+        srcs[(size_t)b * e + i] = row;
+        dsts[(size_t)b * e + i] = row;
+    }
+    if (st != 0)
+        return;
+    // tables: source p (syndrome row), output i: coefficient (V_E^-1)[i][p]
+    uint4* t4 = tabs4 + (size_t)b * tab_block_stride;
+    uint32_t* tc = ctab + (size_t)b * tab_block_stride;
+    for (int idx = tid; idx < e * rows_pad; idx += nt) {
+        const int p = idx / rows_pad, i = idx - p * rows_pad;
+        uint32_t t[5] = {0, 0, 0, 0, 0};
+        if (i < e) {
+            const uint8_t c = Dm[i * n + p];
+            uint8_t v[20];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                v[q] = gmul(c, (uint8_t)q);
+                v[8 + q] = gmul(c, (uint8_t)(q << 3));
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                v[16 + q] = gmul(c, (uint8_t)(q << 6));
+#pragma unroll
+            for (int q = 0; q < 5; ++q)
+                t[q] = (uint32_t)v[4 * q] | ((uint32_t)v[4 * q + 1] << 8) |
+                       ((uint32_t)v[4 * q + 2] << 16) | ((uint32_t)v[4 * q + 3] << 24);
+        }
+        t4[idx] = make_uint4(t[0], t[1], t[2], t[3]);
+        tc[idx] = t[4];
+    }
+}
+
+size_t decode_prepare_syn_lds_bytes(int e) { return 832 + 2 * (size_t)e * e; }
+
+hipError_t launch_decode_prepare_syn(int k, int e, int rows_pad, long long blocks,
+                                     const uint8_t* err, uint8_t* out, long long out_pitch,
+                                     const uint8_t** srcs, uint8_t** dsts, uint4* tabs4,
+                                     uint32_t* ctab, long long tab_block_stride,
+                                     unsigned long long* emask, int* status, hipStream_t st)
+{
+    static bool attr_set = false;
+    if (!attr_set) {
+        (void)hipFuncSetAttribute((const void*)k_decode_prepare_syn,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        attr_set = true;
+    }
+    hipLaunchKernelGGL(k_decode_prepare_syn, dim3((unsigned)blocks), dim3(256),
+                       decode_prepare_syn_lds_bytes(e), st, k, e, rows_pad, err, out, out_pitch,
+                       srcs, dsts, tabs4, ctab, tab_block_stride, emask, status);
     return hipGetLastError();
 }
 

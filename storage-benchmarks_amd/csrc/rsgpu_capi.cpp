@@ -473,7 +473,13 @@ int rsgpu_encode_blocks(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch, 
         return RSGPU_OK;
     const bool aligned = ((uintptr_t)d_src % 16 == 0) && ((uintptr_t)d_parity % 16 == 0) &&
                          (pitch % 16 == 0);
-    // Fast path: the gf_gen_rs_matrix code with compile-time coefficients.
+    // Fast paths: the gf_gen_rs_matrix code with compile-time coefficients,
+    // bit-sliced (len % 32 == 0) or nibble-table (len % 4 == 0).
+    if (!coef && aligned && len % 32 == 0 && rs_bitsliced_available(k, e)) {
+        RS_HIP(ctx, launch_rs_bitsliced(k, e, d_src, nullptr, d_parity, (long long)pitch,
+                                        (long long)len, (long long)blocks, nullptr, ctx->stream));
+        return RSGPU_OK;
+    }
     if (!coef && aligned && len % 4 == 0 && rs_encode_specialized_available(k, e)) {
         RS_HIP(ctx, launch_rs_encode_specialized(k, e, d_src, d_parity, (long long)pitch,
                                                  (long long)len, (long long)blocks, ctx->stream));
@@ -504,11 +510,22 @@ int rsgpu_encode_blocks(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch, 
                                   src_ptr_bytes + dst_ptr_bytes, !aligned);
 }
 
+// Syndrome decode (bit-sliced syndromes + runtime e x e in place) applies to
+// the instantiated codes with 32-byte-multiple rows; otherwise the direct
+// k x k inversion + e x k dot product.
+static bool use_syn_path(int k, int e, size_t len, size_t pitch, const void* src, const void* par,
+                         const void* out)
+{
+    return rs_bitsliced_available(k, e) && len % 32 == 0 && pitch % 16 == 0 &&
+           (uintptr_t)src % 16 == 0 && (uintptr_t)par % 16 == 0 && (uintptr_t)out % 16 == 0;
+}
+
 static void decode_ws_layout(int k, int e, size_t blocks, size_t* off_surv, size_t* off_out,
                              size_t* off_t4, size_t* off_tc, size_t* total)
 {
     const int rows_pad = rows_pad_for(e);
-    size_t o = 0;
+    size_t o = 16 * blocks;  // emask [blocks][2] u64 at offset 0
+    o = align_up(o, 256);
     *off_surv = o;
     o = align_up(o + sizeof(void*) * (size_t)k * blocks, 256);
     *off_out = o;
@@ -545,6 +562,14 @@ int rsgpu_decode_prepare(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch,
     decode_ws_layout(k, e, blocks, &o_surv, &o_out, &o_t4, &o_tc, &total);
     char* ws = (char*)d_workspace;
     const int rows_pad = rows_pad_for(e);
+    if (use_syn_path(k, e, len, pitch, d_src, d_parity, d_out)) {
+        RS_HIP(ctx, launch_decode_prepare_syn(
+                        k, e, rows_pad, (long long)blocks, d_err, d_out, (long long)pitch,
+                        (const uint8_t**)(ws + o_surv), (uint8_t**)(ws + o_out),
+                        (uint4*)(ws + o_t4), (uint32_t*)(ws + o_tc), (long long)e * rows_pad,
+                        (unsigned long long*)ws, d_status, ctx->stream));
+        return RSGPU_OK;
+    }
     PrepArgs p{};
     p.k = k;
     p.e = e;
@@ -582,6 +607,28 @@ int rsgpu_decode_apply(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch, s
     decode_ws_layout(k, e, blocks, &o_surv, &o_out, &o_t4, &o_tc, &total);
     char* ws = (char*)d_workspace;
     const int rows_pad = rows_pad_for(e);
+    if (use_syn_path(k, e, len, pitch, d_src, d_parity, d_out)) {
+        // syndromes into out (blocks with a bad status are computed but then
+        // left alone by the in-place dot product, which skips them)
+        RS_HIP(ctx, launch_rs_bitsliced(k, e, d_src, d_parity, d_out, (long long)pitch,
+                                        (long long)len, (long long)blocks,
+                                        (const uint64_t*)ws, ctx->stream));
+        DotArgs a{};
+        a.srcs = (const uint8_t* const*)(ws + o_surv);
+        a.dsts = (uint8_t* const*)(ws + o_out);
+        a.tabs4 = (const uint4*)(ws + o_t4);
+        a.ctab = (const uint32_t*)(ws + o_tc);
+        a.tab_block_stride = (long long)e * rows_pad;
+        a.k = e;
+        a.rows = e;
+        a.rows_pad = rows_pad;
+        a.len = (long long)len;
+        a.blocks = (long long)blocks;
+        a.status = d_status;
+        a.bytewise = false;
+        RS_HIP(ctx, launch_dot_generic(a, ctx->stream));
+        return RSGPU_OK;
+    }
     const bool aligned = ((uintptr_t)d_src % 16 == 0) && ((uintptr_t)d_parity % 16 == 0) &&
                          ((uintptr_t)d_out % 16 == 0) && (pitch % 16 == 0);
     DotArgs a{};
