@@ -58,6 +58,14 @@ void *rsgpu_get_stream(rsgpu_ctx *ctx);
 int rsgpu_synchronize(rsgpu_ctx *ctx);
 const char *rsgpu_last_error(rsgpu_ctx *ctx);
 
+/* Per-kernel timing (instrumentation, off by default): while enabled every
+ * kernel the engine enqueues is bracketed by HIP events on the context's
+ * stream.  rsgpu_timing_read() synchronises the stream, writes up to `max`
+ * (kernel name, milliseconds) pairs in launch order, returns how many, and
+ * clears the log.  Names are static strings owned by the library. */
+int rsgpu_timing_enable(rsgpu_ctx *ctx, int on);
+int rsgpu_timing_read(rsgpu_ctx *ctx, const char **names, float *ms, int max);
+
 /* Device memory helpers for C/C++ callers without another allocator. */
 int rsgpu_malloc(rsgpu_ctx *ctx, void **dptr, size_t bytes);
 int rsgpu_free(rsgpu_ctx *ctx, void *dptr);

@@ -25,6 +25,14 @@ struct rsgpu_ctx {
     size_t stage_bytes = 0;
     hipEvent_t stage_done = nullptr;
     bool stage_pending = false;
+    // timing instrumentation
+    bool timing = false;
+    struct Rec {
+        const char* name;
+        hipEvent_t a, b;
+    };
+    std::vector<Rec> recs;
+    std::vector<hipEvent_t> ev_pool;
 };
 
 namespace {
@@ -107,6 +115,40 @@ int upload(rsgpu_ctx* ctx, void* d_dst, size_t bytes)
 
 inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
+hipEvent_t pool_event(rsgpu_ctx* ctx)
+{
+    if (!ctx->ev_pool.empty()) {
+        hipEvent_t e = ctx->ev_pool.back();
+        ctx->ev_pool.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    (void)hipEventCreate(&e);
+    return e;
+}
+
+// Brackets one kernel launch with events when timing is enabled.
+struct KTimer {
+    rsgpu_ctx* ctx;
+    rsgpu_ctx::Rec rec{};
+    KTimer(rsgpu_ctx* c, const char* name) : ctx(c)
+    {
+        if (!ctx->timing)
+            return;
+        rec.name = name;
+        rec.a = pool_event(ctx);
+        rec.b = pool_event(ctx);
+        (void)hipEventRecord(rec.a, ctx->stream);
+    }
+    ~KTimer()
+    {
+        if (!ctx->timing)
+            return;
+        (void)hipEventRecord(rec.b, ctx->stream);
+        ctx->recs.push_back(rec);
+    }
+};
+
 // Fill host tables [k][rows_pad] for coefficient matrix coef[rows][k]
 // (coef row r column j at coef[r*k + j]).
 void fill_tables(const uint8_t* coef, int k, int rows, int rows_pad, uint4* t4, uint32_t* tc)
@@ -161,7 +203,10 @@ int generic_from_host_coef(rsgpu_ctx* ctx, const uint8_t* coef, int k, int rows,
     a.blocks = blocks;
     a.status = nullptr;
     a.bytewise = bytewise;
-    RS_HIP(ctx, launch_dot_generic(a, ctx->stream));
+    {
+        KTimer kt(ctx, "k_dot_generic");
+        RS_HIP(ctx, launch_dot_generic(a, ctx->stream));
+    }
     return RSGPU_OK;
 }
 
@@ -200,6 +245,12 @@ int rsgpu_destroy(rsgpu_ctx* ctx)
         (void)hipHostFree(ctx->h_stage);
     if (ctx->stage_done)
         (void)hipEventDestroy(ctx->stage_done);
+    for (auto& r : ctx->recs) {
+        (void)hipEventDestroy(r.a);
+        (void)hipEventDestroy(r.b);
+    }
+    for (auto e : ctx->ev_pool)
+        (void)hipEventDestroy(e);
     delete ctx;
     return RSGPU_OK;
 }
@@ -223,6 +274,37 @@ int rsgpu_synchronize(rsgpu_ctx* ctx)
 }
 
 const char* rsgpu_last_error(rsgpu_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int rsgpu_timing_enable(rsgpu_ctx* ctx, int on)
+{
+    if (!ctx)
+        return RSGPU_ERR_ARG;
+    ctx->timing = on != 0;
+    return RSGPU_OK;
+}
+
+int rsgpu_timing_read(rsgpu_ctx* ctx, const char** names, float* ms, int max)
+{
+    if (!ctx || max < 0)
+        return RSGPU_ERR_ARG;
+    RS_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    int n = 0;
+    for (auto& r : ctx->recs) {
+        if (n < max) {
+            float t = 0;
+            (void)hipEventElapsedTime(&t, r.a, r.b);
+            if (names)
+                names[n] = r.name;
+            if (ms)
+                ms[n] = t;
+            ++n;
+        }
+        ctx->ev_pool.push_back(r.a);
+        ctx->ev_pool.push_back(r.b);
+    }
+    ctx->recs.clear();
+    return n;
+}
 
 int rsgpu_malloc(rsgpu_ctx* ctx, void** p, size_t bytes)
 {
@@ -476,11 +558,13 @@ int rsgpu_encode_blocks(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch, 
     // Fast paths: the gf_gen_rs_matrix code with compile-time coefficients,
     // bit-sliced (len % 32 == 0) or nibble-table (len % 4 == 0).
     if (!coef && aligned && len % 32 == 0 && rs_bitsliced_available(k, e)) {
+        KTimer kt(ctx, "k_rs_bs(encode)");
         RS_HIP(ctx, launch_rs_bitsliced(k, e, d_src, nullptr, d_parity, (long long)pitch,
                                         (long long)len, (long long)blocks, nullptr, ctx->stream));
         return RSGPU_OK;
     }
     if (!coef && aligned && len % 4 == 0 && rs_encode_specialized_available(k, e)) {
+        KTimer kt(ctx, "k_rs_encode_lh");
         RS_HIP(ctx, launch_rs_encode_specialized(k, e, d_src, d_parity, (long long)pitch,
                                                  (long long)len, (long long)blocks, ctx->stream));
         return RSGPU_OK;
@@ -563,6 +647,7 @@ int rsgpu_decode_prepare(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch,
     char* ws = (char*)d_workspace;
     const int rows_pad = rows_pad_for(e);
     if (use_syn_path(k, e, len, pitch, d_src, d_parity, d_out)) {
+        KTimer kt(ctx, "k_decode_prepare_syn");
         RS_HIP(ctx, launch_decode_prepare_syn(
                         k, e, rows_pad, (long long)blocks, d_err, d_out, (long long)pitch,
                         (const uint8_t**)(ws + o_surv), (uint8_t**)(ws + o_out),
@@ -588,6 +673,7 @@ int rsgpu_decode_prepare(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch,
     p.ctab = (uint32_t*)(ws + o_tc);
     p.tab_block_stride = (long long)k * rows_pad;
     p.status = d_status;
+    KTimer kt(ctx, "k_decode_prepare");
     RS_HIP(ctx, launch_decode_prepare(p, ctx->stream));
     return RSGPU_OK;
 }
@@ -610,9 +696,12 @@ int rsgpu_decode_apply(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch, s
     if (use_syn_path(k, e, len, pitch, d_src, d_parity, d_out)) {
         // syndromes into out (blocks with a bad status are computed but then
         // left alone by the in-place dot product, which skips them)
-        RS_HIP(ctx, launch_rs_bitsliced(k, e, d_src, d_parity, d_out, (long long)pitch,
-                                        (long long)len, (long long)blocks,
-                                        (const uint64_t*)ws, ctx->stream));
+        {
+            KTimer kt(ctx, "k_rs_bs(syndrome)");
+            RS_HIP(ctx, launch_rs_bitsliced(k, e, d_src, d_parity, d_out, (long long)pitch,
+                                            (long long)len, (long long)blocks,
+                                            (const uint64_t*)ws, ctx->stream));
+        }
         DotArgs a{};
         a.srcs = (const uint8_t* const*)(ws + o_surv);
         a.dsts = (uint8_t* const*)(ws + o_out);
@@ -626,6 +715,7 @@ int rsgpu_decode_apply(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch, s
         a.blocks = (long long)blocks;
         a.status = d_status;
         a.bytewise = false;
+        KTimer kt(ctx, "k_dot_generic(solve)");
         RS_HIP(ctx, launch_dot_generic(a, ctx->stream));
         return RSGPU_OK;
     }
@@ -644,6 +734,7 @@ int rsgpu_decode_apply(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch, s
     a.blocks = (long long)blocks;
     a.status = d_status;
     a.bytewise = !aligned;
+    KTimer kt(ctx, "k_dot_generic(decode)");
     RS_HIP(ctx, launch_dot_generic(a, ctx->stream));
     return RSGPU_OK;
 }
