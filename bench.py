@@ -53,9 +53,73 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-threads", type=int, default=None)
     p.add_argument("--no-verify", action="store_true")
+    p.add_argument("--host-io", type=int, default=0, metavar="BLOCKS",
+                   help="also time the host-resident path (H2D + kernel + D2H) on BLOCKS blocks")
     p.add_argument("--traffic", default=None,
                    help="JSON with PMC-derived HBM bytes per launch (profiles/)")
     return p.parse_args()
+
+
+def shard(rank: int, blocks_per_rank: int):
+    """Blocks owned by `rank`: [rank*B, (rank+1)*B) -- independent blocks, no
+    exchange between ranks; weak scaling."""
+    return rank * blocks_per_rank, blocks_per_rank
+
+
+def reduce_max_time(elapsed: float, world: int, device) -> float:
+    """Max over ranks of the timed region (the slowest rank bounds the job)."""
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def job_goodput(out_bytes_per_rank_step: float, steps: int, world: int, elapsed: float) -> float:
+    """Whole-job goodput in GiB/s: all ranks' output bytes / max-rank time."""
+    return out_bytes_per_rank_step * steps * world / elapsed / 2 ** 30
+
+
+def host_io_rate(rsgpu, ctx, k, e, L, blocks, seed, reps=3):
+    """Goodput when the blocks start and end in (pinned) host memory, as the
+    reference's buffers do: encode = H2D(sources) + encode + D2H(parity);
+    decode = H2D(survivors + parity) + decode + D2H(recovered).  Returns
+    GiB/s of output bytes over the summed wall time (median of reps)."""
+    import torch
+    enc = rsgpu.GpuEncoder(k, L, e, blocks=blocks, seed=seed, ctx=ctx)
+    dec = rsgpu.GpuDecoder(k, L, e, blocks=blocks, seed=seed, ctx=ctx)
+    h_src = torch.empty(enc.src.numel(), dtype=torch.uint8, pin_memory=True)
+    h_par = torch.empty(enc.par.numel(), dtype=torch.uint8, pin_memory=True)
+    h_out = torch.empty(dec.out.numel(), dtype=torch.uint8, pin_memory=True)
+    h_src.copy_(enc.src)
+    h_par.copy_(enc.par)
+    torch.cuda.synchronize()
+    times = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        enc.src.copy_(h_src, non_blocking=True)
+        enc.encode_all()
+        h_par.copy_(enc.par, non_blocking=True)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        # decoder side: survivors (all source rows are shipped; the erased ones
+        # are simply not read) + parity in, recovered rows out
+        enc.src.copy_(h_src, non_blocking=True)
+        enc.par.copy_(h_par, non_blocking=True)
+        dec.decode_all(enc)
+        h_out.copy_(dec.out, non_blocking=True)
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        times.append((t1 - t0, t2 - t1))
+    times.sort(key=lambda x: x[0] + x[1])
+    te, td = times[len(times) // 2]
+    ok = dec.is_complete() and dec.verify_data(enc)
+    out_b = e * L * blocks
+    return {"blocks": blocks, "encode_s": te, "decode_s": td,
+            "goodput_GiBps": 2 * out_b / (te + td) / 2 ** 30,
+            "encode_GiBps": out_b / te / 2 ** 30, "decode_GiBps": out_b / td / 2 ** 30,
+            "verified": ok}
 
 
 def dist_env():
@@ -109,8 +173,9 @@ def main():
     ctx.set_torch_stream()
 
     # rank r owns global blocks [r*B, (r+1)*B): independent shard, no exchange
-    enc = rsgpu.GpuEncoder(k, L, e, blocks=B, seed=args.seed, ctx=ctx, block0=rank * B)
-    dec = rsgpu.GpuDecoder(k, L, e, blocks=B, seed=args.seed, ctx=ctx, block0=rank * B)
+    blk0, B = shard(rank, B)
+    enc = rsgpu.GpuEncoder(k, L, e, blocks=B, seed=args.seed, ctx=ctx, block0=blk0)
+    dec = rsgpu.GpuDecoder(k, L, e, blocks=B, seed=args.seed, ctx=ctx, block0=blk0)
     torch.cuda.synchronize()
 
     # Per-kernel HIP events: the engine brackets every launch on its stream
@@ -142,18 +207,14 @@ def main():
     ctx.timing_enable(False)
     if world > 1:
         dist.barrier()
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = float(t.item())
+    elapsed = reduce_max_time(elapsed, world, dev)
 
     ok = True
     if not args.no_verify:
         ok = dec.is_complete() and dec.verify_data(enc)
 
     out_bytes_step = 2.0 * e * L * B            # parity + recovered, per rank
-    total_out = out_bytes_step * args.steps * world
-    value = total_out / elapsed / 2 ** 30
+    value = job_goodput(out_bytes_step, args.steps, world, elapsed)
     ms_step = elapsed / args.steps * 1e3
     op_bytes = float((k + e) * L * B)           # one encode or one decode: read k, write e rows
     # algorithmic HBM bytes per launch of each kernel
@@ -198,6 +259,8 @@ def main():
                      "alg_bytes_per_launch": alg.get(dom, 0.0), "avg_ms": round(dom_ms, 3)},
         "cpu_baseline": None,
     }
+    if args.host_io and rank == 0:
+        line["host_io"] = host_io_rate(rsgpu, ctx, k, e, L, args.host_io, args.seed)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = args.cpu_threads or min(16, os.cpu_count() or 1)
         try:

@@ -240,3 +240,20 @@ def test_throughput_benchmark_mirror(ctx):
     for c in cfgs:
         row = tb.run(c)
         assert row["accepted"] and row["goodput"] > 0
+
+
+def test_cpp_runner_end_to_end(tmp_path):
+    """The C++ plugin + harness (storage-benchmarks_amd/host) on the GPU, with
+    gauge-compatible CSV output columns."""
+    import subprocess
+    runner = os.path.join(os.path.dirname(HERE), "storage-benchmarks_amd", "bin", "rs_throughput")
+    csv_path = tmp_path / "out.csv"
+    r = subprocess.run([runner, "--symbols", "16", "64", "--symbol_size", "64000",
+                        "--loss_rate", "0.5", "--blocks", "4", "--runs", "2",
+                        "--csv_file", str(csv_path)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    lines = csv_path.read_text().strip().splitlines()
+    assert lines[0].startswith("testcase,benchmark,symbols,symbol_size,loss_rate,type,erased_symbols")
+    assert len(lines) == 1 + 2 * 2 * 2  # symbols x type x runs
+    for ln in lines[1:]:
+        assert float(ln.split(",")[-1]) > 0

@@ -1,0 +1,49 @@
+"""Host-side harness logic (no GPU): the configuration cross-product and
+erased-symbol count of throughput_benchmark::get_options
+(benchmark/throughput_benchmark.hpp:126-163) as restated by
+rsgpu.ThroughputBenchmark, and the C++ runner's option handling."""
+import math
+import os
+import subprocess
+
+import pytest
+
+import rsgpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+RUNNER = os.path.join(ROOT, "storage-benchmarks_amd", "bin", "rs_throughput")
+
+
+def test_cross_product_order_and_erased():
+    tb = rsgpu.ThroughputBenchmark(symbols=(16, 64), loss_rate=(0.5, 0.2),
+                                   symbol_size=(32000, 1000000), types=("encoder", "decoder"))
+    cfgs = tb.configurations()
+    assert len(cfgs) == 2 * 2 * 2 * 2
+    # nesting: symbols > loss_rate > symbol_size > type (hpp:137-160)
+    assert [(c.symbols, c.loss_rate, c.symbol_size, c.type) for c in cfgs[:4]] == [
+        (16, 0.5, 32000, "encoder"), (16, 0.5, 32000, "decoder"),
+        (16, 0.5, 1000000, "encoder"), (16, 0.5, 1000000, "decoder")]
+    for c in cfgs:
+        assert c.erased_symbols == math.ceil(c.symbols * c.loss_rate)  # hpp:155
+
+
+def test_reference_defaults():
+    # isa.cpp:261-308 defaults: symbols=16, loss_rate=0.5, symbol_size=1e6, both types
+    tb = rsgpu.ThroughputBenchmark()
+    cfgs = tb.configurations()
+    assert [(c.symbols, c.loss_rate, c.symbol_size, c.erased_symbols, c.type) for c in cfgs] == [
+        (16, 0.5, 1000000, 8, "encoder"), (16, 0.5, 1000000, 8, "decoder")]
+
+
+def test_symbol_size_must_be_multiple_of_64():
+    tb = rsgpu.ThroughputBenchmark(symbol_size=(1000,))
+    with pytest.raises(AssertionError):
+        tb.configurations()
+
+
+@pytest.mark.skipif(not os.path.exists(RUNNER), reason="runner not built")
+def test_cpp_runner_usage():
+    r = subprocess.run([RUNNER, "--help"], capture_output=True, text=True)
+    assert r.returncode == 0 and "--symbols" in r.stdout
+    r = subprocess.run([RUNNER, "--bogus"], capture_output=True, text=True)
+    assert r.returncode == 2
