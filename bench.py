@@ -217,24 +217,32 @@ def main():
     value = job_goodput(out_bytes_step, args.steps, world, elapsed)
     ms_step = elapsed / args.steps * 1e3
     op_bytes = float((k + e) * L * B)           # one encode or one decode: read k, write e rows
-    # algorithmic HBM bytes per launch of each kernel
-    alg = {"k_rs_bs(encode)": op_bytes, "k_rs_encode_lh": op_bytes, "k_dot_generic": op_bytes,
-           "k_rs_bs(syndrome)": op_bytes, "k_dot_generic(decode)": op_bytes,
-           "k_dot_generic(solve)": 2.0 * e * L * B,
+    # algorithmic HBM bytes per BLOCK of each kernel; a
+    # launch covers the number of blocks the engine recorded for it (the
+    # decode runs in block chunks on two streams)
+    blk_op = float((k + e) * L)
+    alg = {"k_rs_bs(encode)": blk_op, "k_rs_encode_lh": blk_op, "k_dot_generic": blk_op,
+           "k_rs_bs(syndrome)": blk_op, "k_dot_generic(decode)": blk_op,
+           "k_dot_generic(solve)": 2.0 * e * L, "k_rs_tc(solve)": 2.0 * e * L,
            "k_decode_prepare": 0.0, "k_decode_prepare_syn": 0.0}
     per = {}
-    for name, ms in recs:
-        d = per.setdefault(name, [0.0, 0])
+    for name, ms, nb in recs:
+        d = per.setdefault(name, [0.0, 0, 0])
         d[0] += ms
         d[1] += 1
+        d[2] += nb
     kernels = {}
-    for name, (tot, n) in per.items():
-        avg = tot / n
-        kernels[name] = {"avg_ms": round(avg, 3), "launches": n,
-                         "alg_GBps": round(alg.get(name, 0.0) / (avg * 1e-3) / 1e9, 1)}
-    dom = max(per, key=lambda n: per[n][0] / per[n][1])
-    dom_ms = per[dom][0] / per[dom][1]
-    achieved = alg.get(dom, 0.0) / (dom_ms * 1e-3) / 1e9
+    for name, (tot, n, nb) in per.items():
+        kernels[name] = {"avg_ms": round(tot / n, 3), "launches": n,
+                         "blocks_per_launch": nb / n,
+                         "alg_GBps": round(alg.get(name, 0.0) * nb / (tot * 1e-3) / 1e9, 1),
+                         "ms_per_step": round(tot / args.steps, 3)}
+    # dominant kernel = the most device time per step
+    dom = max(per, key=lambda n: per[n][0])
+    tot, n, nb = per[dom]
+    dom_ms = tot / n
+    dom_bytes = alg.get(dom, 0.0) * nb / n      # algorithmic bytes per launch
+    achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
     traffic = None
     if args.traffic and os.path.exists(args.traffic):
         traffic = json.load(open(args.traffic)).get(dom)
@@ -256,7 +264,7 @@ def main():
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
-                     "alg_bytes_per_launch": alg.get(dom, 0.0), "avg_ms": round(dom_ms, 3)},
+                     "alg_bytes_per_launch": dom_bytes, "avg_ms": round(dom_ms, 3)},
         "cpu_baseline": None,
     }
     if args.host_io and rank == 0:

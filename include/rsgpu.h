@@ -59,12 +59,14 @@ int rsgpu_synchronize(rsgpu_ctx *ctx);
 const char *rsgpu_last_error(rsgpu_ctx *ctx);
 
 /* Per-kernel timing (instrumentation, off by default): while enabled every
- * kernel the engine enqueues is bracketed by HIP events on the context's
- * stream.  rsgpu_timing_read() synchronises the stream, writes up to `max`
- * (kernel name, milliseconds) pairs in launch order, returns how many, and
+ * kernel the engine enqueues is bracketed by HIP events on the stream it runs
+ * on.  rsgpu_timing_read() synchronises the streams, writes up to `max`
+ * (kernel name, milliseconds, blocks processed) records in launch order
+ * (any output array may be NULL), returns how many, and
  * clears the log.  Names are static strings owned by the library. */
 int rsgpu_timing_enable(rsgpu_ctx *ctx, int on);
-int rsgpu_timing_read(rsgpu_ctx *ctx, const char **names, float *ms, int max);
+int rsgpu_timing_read(rsgpu_ctx *ctx, const char **names, float *ms, size_t *blocks,
+                      int max);
 
 /* Device memory helpers for C/C++ callers without another allocator. */
 int rsgpu_malloc(rsgpu_ctx *ctx, void **dptr, size_t bytes);
@@ -135,7 +137,9 @@ int rsgpu_decode_blocks(rsgpu_ctx *ctx, int k, int e, size_t len, size_t pitch, 
  * prepare = survivor matrix + gf_invert_matrix + decode tables + row pointers
  * (isa.cpp:177-207) into d_workspace and d_status; apply = the dot product
  * (isa.cpp:208-209) for blocks whose status is 0.  decode_blocks ==
- * prepare followed by apply on the same stream. */
+ * prepare followed by apply on the same stream.  apply may fan work out to an
+ * internal second stream; it always joins back, so everything it wrote is
+ * ordered before later work on the context stream. */
 int rsgpu_decode_prepare(rsgpu_ctx *ctx, int k, int e, size_t len, size_t pitch, size_t blocks,
                          const unsigned char *d_src, const unsigned char *d_parity,
                          const unsigned char *d_err, unsigned char *d_out, void *d_workspace,

@@ -1,0 +1,87 @@
+// bitslice.h -- device helpers shared by the bit-sliced kernels
+// (rs_bitsliced.hip: compile-time coefficients; rs_tc.hip: runtime
+// coefficients through threaded-code handlers).  A lane holds 32 consecutive
+// bytes of a row; tr8 turns its 8 dwords into 8 bit-planes and back.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace rsgpu {
+namespace bs {
+
+__device__ __forceinline__ uint32_t x3(uint32_t a, uint32_t b, uint32_t c)
+{
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+
+// Opaque VGPR copy of a constant: keeps masks out of SGPR operands (an SGPR
+// operand makes v_bitop3 a 4-cycle issue, profiles/r1_ubench_valu.log).
+__device__ __forceinline__ uint32_t vconst(uint32_t c)
+{
+    uint32_t v;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(v) : "i"(c));
+    return v;
+}
+
+// (lo, hi) block swap of the SWAR 8x8 bit transpose, per byte lane:
+//   lo' = (lo & m) | ((hi << s) & ~m),  hi' = ((lo >> s) & m) | (hi & ~m)
+// bitop3 truth tables (src0=0xF0, src1=0xCC, src2=0xAA):
+//   f(a, b, m) = (a & m) | (b & ~m)  -> (0xF0 & 0xAA) | (0xCC & 0x55) = 0xE4
+template <int S>
+__device__ __forceinline__ void swap_blk(uint32_t& lo, uint32_t& hi, uint32_t m)
+{
+    const uint32_t hs = hi << S;
+    const uint32_t ls = lo >> S;
+    const uint32_t nl = __builtin_amdgcn_bitop3_b32(lo, hs, m, 0xE4);
+    const uint32_t nh = __builtin_amdgcn_bitop3_b32(ls, hi, m, 0xE4);
+    lo = nl;
+    hi = nh;
+}
+
+// In place: W[w] byte q = byte (4w+q) of a 32-byte segment  <->  plane
+// layout W[a] byte q bit w = bit a of that byte.  Self-inverse.
+__device__ __forceinline__ void tr8(uint32_t (&W)[8], uint32_t m4, uint32_t m2, uint32_t m1)
+{
+    swap_blk<4>(W[0], W[4], m4);
+    swap_blk<4>(W[1], W[5], m4);
+    swap_blk<4>(W[2], W[6], m4);
+    swap_blk<4>(W[3], W[7], m4);
+    swap_blk<2>(W[0], W[2], m2);
+    swap_blk<2>(W[1], W[3], m2);
+    swap_blk<2>(W[4], W[6], m2);
+    swap_blk<2>(W[5], W[7], m2);
+    swap_blk<1>(W[0], W[1], m1);
+    swap_blk<1>(W[2], W[3], m1);
+    swap_blk<1>(W[4], W[5], m1);
+    swap_blk<1>(W[6], W[7], m1);
+}
+
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) const v4u gcv4u;
+typedef __attribute__((address_space(1))) v4u gv4u;
+
+__device__ __forceinline__ void load32(const uint8_t* row, long long off, bool ok, uint32_t (&W)[8])
+{
+    if (ok) {
+        const v4u a = *(gcv4u*)(row + off);
+        const v4u b = *(gcv4u*)(row + off + 16);
+        W[0] = a.x; W[1] = a.y; W[2] = a.z; W[3] = a.w;
+        W[4] = b.x; W[5] = b.y; W[6] = b.z; W[7] = b.w;
+    } else {
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+            W[i] = 0;
+    }
+}
+
+__device__ __forceinline__ void store32(uint8_t* row, long long off, const uint32_t (&W)[8])
+{
+    v4u a, b;
+    a.x = W[0]; a.y = W[1]; a.z = W[2]; a.w = W[3];
+    b.x = W[4]; b.y = W[5]; b.z = W[6]; b.w = W[7];
+    *(gv4u*)(row + off) = a;
+    *(gv4u*)(row + off + 16) = b;
+}
+
+}  // namespace bs
+}  // namespace rsgpu

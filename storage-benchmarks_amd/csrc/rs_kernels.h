@@ -54,11 +54,35 @@ hipError_t launch_rs_bitsliced(int k, int e, const uint8_t* src, const uint8_t* 
                                long long pitch, long long len, long long blocks,
                                const uint64_t* emask, hipStream_t st);
 
+// Syndrome-decode prepare: per block, emask, V_E^-1 and its consumers' tables:
+// k_dot_generic tables (tabs4/ctab, when non-null) and/or k_rs_tc handler
+// addresses (tc_addr [B][e][tc_rows], when non-null; tc_table = the 256
+// handler addresses).
 hipError_t launch_decode_prepare_syn(int k, int e, int rows_pad, long long blocks,
                                      const uint8_t* err, uint8_t* out, long long out_pitch,
                                      const uint8_t** srcs, uint8_t** dsts, uint4* tabs4,
                                      uint32_t* ctab, long long tab_block_stride,
+                                     const unsigned long long* tc_table,
+                                     unsigned long long* tc_addr, int tc_rows,
                                      unsigned long long* emask, int* status, hipStream_t st);
+
+// Threaded-code bit-sliced dot product with runtime coefficients (rs_tc.hip):
+// dsts[b][i] = sum_p c_b[i][p] * srcs[b][p] for rows <= 32, where the
+// coefficients arrive as handler addresses addr[b][p][slot] (slot < tc_rows,
+// padding slots point at handler 0).  len % 32 == 0, 16-byte aligned rows;
+// blocks with status != 0 are skipped.
+struct TcArgs {
+    const uint8_t* const* srcs;      // [B][k]
+    uint8_t* const* dsts;            // [B][rows]
+    const unsigned long long* addr;  // [B][k][tc_rows_per_pass(rows)]
+    int k, rows;
+    long long len;
+    const int* status;               // [B] or nullptr
+};
+int tc_rows_per_pass(int rows);
+int tc_handler_stride();
+hipError_t tc_query_handlers(unsigned long long* d_out, hipStream_t st);
+hipError_t launch_rs_tc(const TcArgs& a, long long blocks, hipStream_t st);
 
 hipError_t launch_row_ptrs(const uint8_t* base, long long pitch, int rows_per_block,
                            long long blocks, const uint8_t** out, hipStream_t st);

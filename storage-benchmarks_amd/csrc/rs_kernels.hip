@@ -818,6 +818,8 @@ __global__ __launch_bounds__(256) void k_decode_prepare_syn(int k, int e, int ro
                                                             const uint8_t** srcs, uint8_t** dsts,
                                                             uint4* tabs4, uint32_t* ctab,
                                                             long long tab_block_stride,
+                                                            const unsigned long long* tc_table,
+                                                            unsigned long long* tc_addr, int tc_rows,
                                                             unsigned long long* emask, int* status)
 {
     extern __shared__ __align__(16) uint8_t lds[];
@@ -941,6 +943,17 @@ __global__ __launch_bounds__(256) void k_decode_prepare_syn(int k, int e, int ro
     }
     if (st != 0)
         return;
+    if (tc_addr) {
+        // handler addresses [p][slot]: coefficient (V_E^-1)[slot][p], padding
+        // slots -> handler 0 (no-op)
+        unsigned long long* ta = tc_addr + (size_t)b * e * tc_rows;
+        for (int idx = tid; idx < e * tc_rows; idx += nt) {
+            const int p = idx / tc_rows, i = idx - p * tc_rows;
+            ta[idx] = tc_table[i < e ? Dm[i * n + p] : 0];
+        }
+    }
+    if (!tabs4)
+        return;
     // tables: source p (syndrome row), output i: coefficient (V_E^-1)[i][p]
     uint4* t4 = tabs4 + (size_t)b * tab_block_stride;
     uint32_t* tc = ctab + (size_t)b * tab_block_stride;
@@ -974,6 +987,8 @@ hipError_t launch_decode_prepare_syn(int k, int e, int rows_pad, long long block
                                      const uint8_t* err, uint8_t* out, long long out_pitch,
                                      const uint8_t** srcs, uint8_t** dsts, uint4* tabs4,
                                      uint32_t* ctab, long long tab_block_stride,
+                                     const unsigned long long* tc_table,
+                                     unsigned long long* tc_addr, int tc_rows,
                                      unsigned long long* emask, int* status, hipStream_t st)
 {
     static bool attr_set = false;
@@ -984,7 +999,8 @@ hipError_t launch_decode_prepare_syn(int k, int e, int rows_pad, long long block
     }
     hipLaunchKernelGGL(k_decode_prepare_syn, dim3((unsigned)blocks), dim3(256),
                        decode_prepare_syn_lds_bytes(e), st, k, e, rows_pad, err, out, out_pitch,
-                       srcs, dsts, tabs4, ctab, tab_block_stride, emask, status);
+                       srcs, dsts, tabs4, ctab, tab_block_stride, tc_table, tc_addr, tc_rows,
+                       emask, status);
     return hipGetLastError();
 }
 

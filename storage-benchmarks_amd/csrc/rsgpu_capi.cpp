@@ -3,7 +3,9 @@
 // batched encode / decode hot path.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -16,6 +18,16 @@
 struct rsgpu_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
+    // second stream for the pipelined decode (syndrome chunk i+1 overlaps the
+    // solve of chunk i); created on first use, joined back into `stream`
+    hipStream_t aux = nullptr;
+    int decode_chunks = 1;
+    std::vector<hipEvent_t> sync_evs;
+    size_t sync_next = 0;
+    // threaded-code solve (rs_tc.hip): device table of the 256 handler
+    // addresses; tc_state 0 = not probed, 1 = ready, -1 = unavailable
+    unsigned long long* d_tc_table = nullptr;
+    int tc_state = 0;
     std::string err;
     // grow-only device scratch for pointer tables / coefficient tables
     void* d_scratch = nullptr;
@@ -30,6 +42,7 @@ struct rsgpu_ctx {
     struct Rec {
         const char* name;
         hipEvent_t a, b;
+        size_t blocks;
     };
     std::vector<Rec> recs;
     std::vector<hipEvent_t> ev_pool;
@@ -127,24 +140,54 @@ hipEvent_t pool_event(rsgpu_ctx* ctx)
     return e;
 }
 
+// Cross-stream ordering events (timing disabled), recycled round-robin: an
+// event may be re-recorded once the stream that waits on it has been handed
+// the wait, which hipStreamWaitEvent captures at enqueue time.
+hipEvent_t sync_event(rsgpu_ctx* ctx)
+{
+    if (ctx->sync_evs.size() < 32) {
+        hipEvent_t e = nullptr;
+        (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
+        ctx->sync_evs.push_back(e);
+        return e;
+    }
+    hipEvent_t e = ctx->sync_evs[ctx->sync_next];
+    ctx->sync_next = (ctx->sync_next + 1) % ctx->sync_evs.size();
+    return e;
+}
+
+// Number of block chunks for the two-stream decode: 1 (no overlap) for small
+// batches; RSGPU_DECODE_CHUNKS overrides for experiments.
+size_t decode_chunk_count(rsgpu_ctx* ctx, size_t blocks)
+{
+    size_t want = (size_t)ctx->decode_chunks;
+    if (const char* v = std::getenv("RSGPU_DECODE_CHUNKS"))
+        want = (size_t)std::max(1, std::atoi(v));
+    const size_t by_size = blocks / 32;  // keep >= 32 blocks per chunk
+    return std::max<size_t>(1, std::min(want, by_size));
+}
+
 // Brackets one kernel launch with events when timing is enabled.
 struct KTimer {
     rsgpu_ctx* ctx;
+    hipStream_t s;
     rsgpu_ctx::Rec rec{};
-    KTimer(rsgpu_ctx* c, const char* name) : ctx(c)
+    KTimer(rsgpu_ctx* c, const char* name, size_t blocks, hipStream_t st = nullptr)
+        : ctx(c), s(st ? st : c->stream)
     {
         if (!ctx->timing)
             return;
         rec.name = name;
+        rec.blocks = blocks;
         rec.a = pool_event(ctx);
         rec.b = pool_event(ctx);
-        (void)hipEventRecord(rec.a, ctx->stream);
+        (void)hipEventRecord(rec.a, s);
     }
     ~KTimer()
     {
         if (!ctx->timing)
             return;
-        (void)hipEventRecord(rec.b, ctx->stream);
+        (void)hipEventRecord(rec.b, s);
         ctx->recs.push_back(rec);
     }
 };
@@ -204,7 +247,7 @@ int generic_from_host_coef(rsgpu_ctx* ctx, const uint8_t* coef, int k, int rows,
     a.status = nullptr;
     a.bytewise = bytewise;
     {
-        KTimer kt(ctx, "k_dot_generic");
+        KTimer kt(ctx, "k_dot_generic", (size_t)blocks);
         RS_HIP(ctx, launch_dot_generic(a, ctx->stream));
     }
     return RSGPU_OK;
@@ -239,6 +282,10 @@ int rsgpu_destroy(rsgpu_ctx* ctx)
         return RSGPU_ERR_ARG;
     (void)hipSetDevice(ctx->device);
     (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->aux) {
+        (void)hipStreamSynchronize(ctx->aux);
+        (void)hipStreamDestroy(ctx->aux);
+    }
     if (ctx->d_scratch)
         (void)hipFree(ctx->d_scratch);
     if (ctx->h_stage)
@@ -251,6 +298,10 @@ int rsgpu_destroy(rsgpu_ctx* ctx)
     }
     for (auto e : ctx->ev_pool)
         (void)hipEventDestroy(e);
+    for (auto e : ctx->sync_evs)
+        (void)hipEventDestroy(e);
+    if (ctx->d_tc_table)
+        (void)hipFree(ctx->d_tc_table);
     delete ctx;
     return RSGPU_OK;
 }
@@ -283,11 +334,13 @@ int rsgpu_timing_enable(rsgpu_ctx* ctx, int on)
     return RSGPU_OK;
 }
 
-int rsgpu_timing_read(rsgpu_ctx* ctx, const char** names, float* ms, int max)
+int rsgpu_timing_read(rsgpu_ctx* ctx, const char** names, float* ms, size_t* blocks, int max)
 {
     if (!ctx || max < 0)
         return RSGPU_ERR_ARG;
     RS_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    if (ctx->aux)
+        RS_HIP(ctx, hipStreamSynchronize(ctx->aux));
     int n = 0;
     for (auto& r : ctx->recs) {
         if (n < max) {
@@ -297,6 +350,8 @@ int rsgpu_timing_read(rsgpu_ctx* ctx, const char** names, float* ms, int max)
                 names[n] = r.name;
             if (ms)
                 ms[n] = t;
+            if (blocks)
+                blocks[n] = r.blocks;
             ++n;
         }
         ctx->ev_pool.push_back(r.a);
@@ -558,13 +613,13 @@ int rsgpu_encode_blocks(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch, 
     // Fast paths: the gf_gen_rs_matrix code with compile-time coefficients,
     // bit-sliced (len % 32 == 0) or nibble-table (len % 4 == 0).
     if (!coef && aligned && len % 32 == 0 && rs_bitsliced_available(k, e)) {
-        KTimer kt(ctx, "k_rs_bs(encode)");
+        KTimer kt(ctx, "k_rs_bs(encode)", blocks);
         RS_HIP(ctx, launch_rs_bitsliced(k, e, d_src, nullptr, d_parity, (long long)pitch,
                                         (long long)len, (long long)blocks, nullptr, ctx->stream));
         return RSGPU_OK;
     }
     if (!coef && aligned && len % 4 == 0 && rs_encode_specialized_available(k, e)) {
-        KTimer kt(ctx, "k_rs_encode_lh");
+        KTimer kt(ctx, "k_rs_encode_lh", blocks);
         RS_HIP(ctx, launch_rs_encode_specialized(k, e, d_src, d_parity, (long long)pitch,
                                                  (long long)len, (long long)blocks, ctx->stream));
         return RSGPU_OK;
@@ -594,6 +649,59 @@ int rsgpu_encode_blocks(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch, 
                                   src_ptr_bytes + dst_ptr_bytes, !aligned);
 }
 
+// Locate the handler table of k_rs_tc once per context: the query kernel
+// reports the table's first and end addresses; the layout must be exactly
+// 256 handlers of tc_handler_stride() bytes, otherwise the threaded-code path
+// stays off (and k_dot_generic solves).
+static int tc_init(rsgpu_ctx* ctx)
+{
+    if (ctx->tc_state != 0)
+        return ctx->tc_state;
+    ctx->tc_state = -1;
+    unsigned long long* d = nullptr;
+    if (hipMalloc((void**)&d, 258 * sizeof(unsigned long long)) != hipSuccess)
+        return -1;
+    unsigned long long se[2] = {0, 0};
+    if (tc_query_handlers(d + 256, ctx->stream) != hipSuccess ||
+        hipMemcpyAsync(se, d + 256, sizeof se, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
+        hipStreamSynchronize(ctx->stream) != hipSuccess) {
+        (void)hipFree(d);
+        return -1;
+    }
+    const unsigned long long stride = (unsigned long long)tc_handler_stride();
+    if (se[0] == 0 || se[1] - se[0] != 256 * stride) {
+        std::fprintf(stderr, "rsgpu: threaded-code handler table has an unexpected layout "
+                             "(%#llx..%#llx); using k_dot_generic\n", se[0], se[1]);
+        (void)hipFree(d);
+        return -1;
+    }
+    unsigned long long h[256];
+    for (int c = 0; c < 256; ++c)
+        h[c] = se[0] + (unsigned long long)c * stride;
+    if (hipMemcpy(d, h, sizeof h, hipMemcpyHostToDevice) != hipSuccess) {
+        (void)hipFree(d);
+        return -1;
+    }
+    ctx->d_tc_table = d;
+    ctx->tc_state = 1;
+    return 1;
+}
+
+// The threaded-code solve serves e <= 32 on the syndrome path.  Decided once
+// per context (RSGPU_NO_TC=1 at first use selects k_dot_generic instead, for
+// comparison), so prepare and apply always agree on the workspace contents.
+static bool use_tc(rsgpu_ctx* ctx, int e)
+{
+    if (e > 32)
+        return false;
+    if (ctx->tc_state == 0) {
+        const char* v = std::getenv("RSGPU_NO_TC");
+        if (v && v[0] == '1')
+            ctx->tc_state = -1;
+    }
+    return tc_init(ctx) == 1;
+}
+
 // Syndrome decode (bit-sliced syndromes + runtime e x e in place) applies to
 // the instantiated codes with 32-byte-multiple rows; otherwise the direct
 // k x k inversion + e x k dot product.
@@ -605,7 +713,7 @@ static bool use_syn_path(int k, int e, size_t len, size_t pitch, const void* src
 }
 
 static void decode_ws_layout(int k, int e, size_t blocks, size_t* off_surv, size_t* off_out,
-                             size_t* off_t4, size_t* off_tc, size_t* total)
+                             size_t* off_t4, size_t* off_tc, size_t* off_tca, size_t* total)
 {
     const int rows_pad = rows_pad_for(e);
     size_t o = 16 * blocks;  // emask [blocks][2] u64 at offset 0
@@ -618,6 +726,8 @@ static void decode_ws_layout(int k, int e, size_t blocks, size_t* off_surv, size
     o = align_up(o + sizeof(uint4) * (size_t)k * rows_pad * blocks, 256);
     *off_tc = o;
     o = align_up(o + sizeof(uint32_t) * (size_t)k * rows_pad * blocks, 256);
+    *off_tca = o;  // k_rs_tc handler addresses [blocks][e][tc_rows]
+    o = align_up(o + sizeof(unsigned long long) * (size_t)e * tc_rows_per_pass(e) * blocks, 256);
     *total = o;
 }
 
@@ -625,8 +735,8 @@ size_t rsgpu_decode_workspace_bytes(int k, int e, size_t blocks)
 {
     if (k <= 0 || e <= 0)
         return 256;
-    size_t a, b, c, d, t;
-    decode_ws_layout(k, e, blocks, &a, &b, &c, &d, &t);
+    size_t a, b, c, d, x, t;
+    decode_ws_layout(k, e, blocks, &a, &b, &c, &d, &x, &t);
     return t;
 }
 
@@ -642,16 +752,19 @@ int rsgpu_decode_prepare(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch,
         return RSGPU_OK;
     if (e > k || !d_err || !d_workspace || !d_status)
         return fail(ctx, RSGPU_ERR_ARG, "rsgpu_decode_prepare: bad arguments");
-    size_t o_surv, o_out, o_t4, o_tc, total;
-    decode_ws_layout(k, e, blocks, &o_surv, &o_out, &o_t4, &o_tc, &total);
+    size_t o_surv, o_out, o_t4, o_tc, o_tca, total;
+    decode_ws_layout(k, e, blocks, &o_surv, &o_out, &o_t4, &o_tc, &o_tca, &total);
     char* ws = (char*)d_workspace;
     const int rows_pad = rows_pad_for(e);
     if (use_syn_path(k, e, len, pitch, d_src, d_parity, d_out)) {
-        KTimer kt(ctx, "k_decode_prepare_syn");
+        const bool tcp = use_tc(ctx, e);
+        KTimer kt(ctx, "k_decode_prepare_syn", blocks);
         RS_HIP(ctx, launch_decode_prepare_syn(
                         k, e, rows_pad, (long long)blocks, d_err, d_out, (long long)pitch,
                         (const uint8_t**)(ws + o_surv), (uint8_t**)(ws + o_out),
-                        (uint4*)(ws + o_t4), (uint32_t*)(ws + o_tc), (long long)e * rows_pad,
+                        tcp ? nullptr : (uint4*)(ws + o_t4), tcp ? nullptr : (uint32_t*)(ws + o_tc),
+                        (long long)e * rows_pad, tcp ? ctx->d_tc_table : nullptr,
+                        tcp ? (unsigned long long*)(ws + o_tca) : nullptr, tc_rows_per_pass(e),
                         (unsigned long long*)ws, d_status, ctx->stream));
         return RSGPU_OK;
     }
@@ -673,7 +786,7 @@ int rsgpu_decode_prepare(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch,
     p.ctab = (uint32_t*)(ws + o_tc);
     p.tab_block_stride = (long long)k * rows_pad;
     p.status = d_status;
-    KTimer kt(ctx, "k_decode_prepare");
+    KTimer kt(ctx, "k_decode_prepare", blocks);
     RS_HIP(ctx, launch_decode_prepare(p, ctx->stream));
     return RSGPU_OK;
 }
@@ -689,34 +802,74 @@ int rsgpu_decode_apply(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch, s
         return RSGPU_OK;
     if (e > k || !d_workspace || !d_status)
         return fail(ctx, RSGPU_ERR_ARG, "rsgpu_decode_apply: bad arguments");
-    size_t o_surv, o_out, o_t4, o_tc, total;
-    decode_ws_layout(k, e, blocks, &o_surv, &o_out, &o_t4, &o_tc, &total);
+    size_t o_surv, o_out, o_t4, o_tc, o_tca, total;
+    decode_ws_layout(k, e, blocks, &o_surv, &o_out, &o_t4, &o_tc, &o_tca, &total);
     char* ws = (char*)d_workspace;
     const int rows_pad = rows_pad_for(e);
     if (use_syn_path(k, e, len, pitch, d_src, d_parity, d_out)) {
-        // syndromes into out (blocks with a bad status are computed but then
-        // left alone by the in-place dot product, which skips them)
-        {
-            KTimer kt(ctx, "k_rs_bs(syndrome)");
-            RS_HIP(ctx, launch_rs_bitsliced(k, e, d_src, d_parity, d_out, (long long)pitch,
-                                            (long long)len, (long long)blocks,
-                                            (const uint64_t*)ws, ctx->stream));
+        // Syndromes into out (bit-sliced, memory-latency bound), then the
+        // in-place e x e solve (VALU bound; blocks with a bad status are
+        // skipped).  The blocks are cut into chunks and the two kernels run
+        // on two streams so that the syndromes of chunk i+1 overlap the solve
+        // of chunk i.
+        const bool tcp = use_tc(ctx, e);
+        const size_t chunks = decode_chunk_count(ctx, blocks);
+        hipStream_t solve_stream = ctx->stream;
+        if (chunks > 1) {
+            if (!ctx->aux)
+                RS_HIP(ctx, hipStreamCreateWithFlags(&ctx->aux, hipStreamNonBlocking));
+            solve_stream = ctx->aux;
         }
-        DotArgs a{};
-        a.srcs = (const uint8_t* const*)(ws + o_surv);
-        a.dsts = (uint8_t* const*)(ws + o_out);
-        a.tabs4 = (const uint4*)(ws + o_t4);
-        a.ctab = (const uint32_t*)(ws + o_tc);
-        a.tab_block_stride = (long long)e * rows_pad;
-        a.k = e;
-        a.rows = e;
-        a.rows_pad = rows_pad;
-        a.len = (long long)len;
-        a.blocks = (long long)blocks;
-        a.status = d_status;
-        a.bytewise = false;
-        KTimer kt(ctx, "k_dot_generic(solve)");
-        RS_HIP(ctx, launch_dot_generic(a, ctx->stream));
+        const size_t per = (blocks + chunks - 1) / chunks;
+        const long long tstride = (long long)e * rows_pad;
+        for (size_t b0 = 0; b0 < blocks; b0 += per) {
+            const size_t nb = std::min(per, blocks - b0);
+            {
+                KTimer kt(ctx, "k_rs_bs(syndrome)", nb);
+                RS_HIP(ctx, launch_rs_bitsliced(k, e, d_src + b0 * k * pitch, d_parity + b0 * e * pitch,
+                                                d_out + b0 * e * pitch, (long long)pitch,
+                                                (long long)len, (long long)nb,
+                                                (const uint64_t*)ws + 2 * b0, ctx->stream));
+            }
+            if (chunks > 1) {
+                hipEvent_t ev = sync_event(ctx);
+                RS_HIP(ctx, hipEventRecord(ev, ctx->stream));
+                RS_HIP(ctx, hipStreamWaitEvent(solve_stream, ev, 0));
+            }
+            if (tcp) {
+                TcArgs t{};
+                t.srcs = (const uint8_t* const*)(ws + o_surv) + b0 * e;
+                t.dsts = (uint8_t* const*)(ws + o_out) + b0 * e;
+                t.addr = (const unsigned long long*)(ws + o_tca) + b0 * e * tc_rows_per_pass(e);
+                t.k = e;
+                t.rows = e;
+                t.len = (long long)len;
+                t.status = d_status + b0;
+                KTimer kt(ctx, "k_rs_tc(solve)", nb, solve_stream);
+                RS_HIP(ctx, launch_rs_tc(t, (long long)nb, solve_stream));
+                continue;
+            }
+            DotArgs a{};
+            a.srcs = (const uint8_t* const*)(ws + o_surv) + b0 * e;
+            a.dsts = (uint8_t* const*)(ws + o_out) + b0 * e;
+            a.tabs4 = (const uint4*)(ws + o_t4) + b0 * tstride;
+            a.ctab = (const uint32_t*)(ws + o_tc) + b0 * tstride;
+            a.tab_block_stride = tstride;
+            a.k = e;
+            a.rows = e;
+            a.rows_pad = rows_pad;
+            a.len = (long long)len;
+            a.blocks = (long long)nb;
+            a.status = d_status + b0;
+            a.bytewise = false;
+            KTimer kt(ctx, "k_dot_generic(solve)", nb, solve_stream);
+            RS_HIP(ctx, launch_dot_generic(a, solve_stream));
+        }
+        if (chunks > 1) {
+            hipEvent_t ev = sync_event(ctx);
+            RS_HIP(ctx, hipEventRecord(ev, solve_stream));
+            RS_HIP(ctx, hipStreamWaitEvent(ctx->stream, ev, 0));
+        }
         return RSGPU_OK;
     }
     const bool aligned = ((uintptr_t)d_src % 16 == 0) && ((uintptr_t)d_parity % 16 == 0) &&
@@ -734,7 +887,7 @@ int rsgpu_decode_apply(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch, s
     a.blocks = (long long)blocks;
     a.status = d_status;
     a.bytewise = !aligned;
-    KTimer kt(ctx, "k_dot_generic(decode)");
+    KTimer kt(ctx, "k_dot_generic(decode)", blocks);
     RS_HIP(ctx, launch_dot_generic(a, ctx->stream));
     return RSGPU_OK;
 }

@@ -59,7 +59,8 @@ _SIGS = {
     "rsgpu_synchronize": (C.c_int, [vp]),
     "rsgpu_last_error": (C.c_char_p, [vp]),
     "rsgpu_timing_enable": (C.c_int, [vp, C.c_int]),
-    "rsgpu_timing_read": (C.c_int, [vp, C.POINTER(C.c_char_p), C.POINTER(C.c_float), C.c_int]),
+    "rsgpu_timing_read": (C.c_int, [vp, C.POINTER(C.c_char_p), C.POINTER(C.c_float),
+                                   C.POINTER(C.c_size_t), C.c_int]),
     "rsgpu_malloc": (C.c_int, [vp, C.POINTER(vp), sz]),
     "rsgpu_free": (C.c_int, [vp, vp]),
     "rsgpu_memcpy_h2d": (C.c_int, [vp, vp, vp, sz]),
@@ -222,13 +223,14 @@ class Context:
         self.check(lib().rsgpu_timing_enable(self._h, 1 if on else 0), "rsgpu_timing_enable")
 
     def timing_read(self, max_records: int = 4096):
-        """[(kernel name, ms)] of the kernels enqueued since the last read."""
+        """[(kernel name, ms, blocks)] of the kernels enqueued since the last read."""
         names = (C.c_char_p * max_records)()
         ms = (C.c_float * max_records)()
-        n = lib().rsgpu_timing_read(self._h, names, ms, max_records)
+        blocks = (C.c_size_t * max_records)()
+        n = lib().rsgpu_timing_read(self._h, names, ms, blocks, max_records)
         if n < 0:
             self.check(n, "rsgpu_timing_read")
-        return [(names[i].decode(), float(ms[i])) for i in range(n)]
+        return [(names[i].decode(), float(ms[i]), int(blocks[i])) for i in range(n)]
 
     def synchronize(self) -> None:
         self.check(lib().rsgpu_synchronize(self._h), "rsgpu_synchronize")
