@@ -27,6 +27,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <utility>
+
 #include "bitslice.h"
 #include "rs_kernels.h"
 #include "tc_handlers.inc"
@@ -34,12 +36,11 @@
 namespace rsgpu {
 namespace tc {
 
-using bs::load32;
 using bs::store32;
 using bs::tr8;
 using bs::vconst;
 
-constexpr int C = 16;  // sources per LDS chunk
+constexpr int C = 8;  // sources per LDS chunk (double-buffered)
 
 // Holds the handler table; launched once per context to report where the
 // table sits (out[0] = first handler, out[1] = end of the table).  The
@@ -72,10 +73,81 @@ __global__ void k_tc_handlers(unsigned long long* out)
     }
 }
 
-template <int NW>
-__global__ __launch_bounds__(64 * NW) void k_rs_tc(TcArgs a)
+// 16 bytes per lane global -> LDS (LDS-DMA, no VGPR destination): lane i's
+// bytes land at lds_byte + 16 i.  M0 holds the LDS base and is restored.
+__device__ __forceinline__ void glds16(const void* g, uint32_t lds_byte)
 {
-    __shared__ uint4 lds[C * 2 * 64];
+    uint32_t keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n"
+        "s_mov_b32 m0, %2\n"
+        "s_nop 0\n"
+        "global_load_lds_dwordx4 %1, off\n"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(g), "s"(lds_byte)
+        : "memory");
+}
+
+// Wave-uniform pointer from a table through the scalar cache.  (hipcc would
+// use a vector load for it -- it cannot prove the table is not written -- and
+// its vmcnt(0) would drain the LDS-DMA in flight.)
+__device__ __forceinline__ const uint8_t* sload_ptr(const uint8_t* const* p)
+{
+    const uint8_t* r;
+    asm volatile("s_load_dwordx2 %0, %1, 0\n s_waitcnt lgkmcnt(0)" : "=s"(r) : "s"(p) : "memory");
+    return r;
+}
+
+// wait until at most N of this wave's vector-memory operations are pending
+__device__ __forceinline__ void wait_vm(int n)
+{
+    switch (n) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+    case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+    case 14: asm volatile("s_waitcnt vmcnt(14)" ::: "memory"); break;
+    case 16: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    }
+}
+
+// workgroup barrier that does not drain the LDS-DMA in flight
+__device__ __forceinline__ void barrier_lds()
+{
+    asm volatile("s_waitcnt lgkmcnt(0)\n s_barrier" ::: "memory");
+}
+
+// Read accumulator slot S (asm-owned v[64+8S : 64+8S+7]) into W.
+template <int S>
+__device__ __forceinline__ void read_slot(uint32_t (&W)[8])
+{
+#define RSGPU_TC_RD(TEXT)                                                                       \
+    asm volatile(TEXT : "=v"(W[0]), "=v"(W[1]), "=v"(W[2]), "=v"(W[3]), "=v"(W[4]), "=v"(W[5]), \
+                        "=v"(W[6]), "=v"(W[7]))
+    if constexpr (S == 0) RSGPU_TC_RD(RSGPU_TC_READ_SLOT0);
+    if constexpr (S == 1) RSGPU_TC_RD(RSGPU_TC_READ_SLOT1);
+    if constexpr (S == 2) RSGPU_TC_RD(RSGPU_TC_READ_SLOT2);
+    if constexpr (S == 3) RSGPU_TC_RD(RSGPU_TC_READ_SLOT3);
+    if constexpr (S == 4) RSGPU_TC_RD(RSGPU_TC_READ_SLOT4);
+    if constexpr (S == 5) RSGPU_TC_RD(RSGPU_TC_READ_SLOT5);
+    if constexpr (S == 6) RSGPU_TC_RD(RSGPU_TC_READ_SLOT6);
+    if constexpr (S == 7) RSGPU_TC_RD(RSGPU_TC_READ_SLOT7);
+#undef RSGPU_TC_RD
+}
+
+// amdgpu_num_vgpr(64): the compiler allocates v0..v63 only; the accumulators
+// v64..v127 are touched by asm alone, so they stay put across the loops (the
+// kernel descriptor still reserves 128 VGPRs because the asm names v127).
+template <int NW>
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_num_vgpr(64))) void k_rs_tc(TcArgs a)
+{
+    // two chunk buffers [C][2 halves][64 lanes] of 16 bytes: 2 x 16 KiB
+    __shared__ uint4 lds[2][C * 2 * 64];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     const int b = blockIdx.y;
@@ -83,55 +155,81 @@ __global__ __launch_bounds__(64 * NW) void k_rs_tc(TcArgs a)
         return;  // uniform per workgroup: the whole block is skipped
     const long long off = (long long)blockIdx.x * 2048 + lane * 32;
     const bool inb = off + 32 <= a.len;
+    const long long loff = inb ? off : 0;  // out-of-range lanes re-read the row head
     const int k = a.k;
+    const int nch = (k + C - 1) / C;
     const uint8_t* const* srcs = a.srcs + (size_t)b * k;
     // addresses [B][k][NW*8]: this wave's 8 slots of source j at ap + j*NW*8
     const unsigned long long* ap = a.addr + (size_t)b * k * (NW * 8) + wave * 8;
     const uint32_t m4 = vconst(0x0F0F0F0Fu), m2 = vconst(0x33333333u), m1 = vconst(0x55555555u);
+    const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint4*)&lds[0][0];
 
-    uint32_t acc[64];
-#pragma unroll
-    for (int i = 0; i < 64; ++i)
-        acc[i] = 0;
-
-    for (int c0 = 0; c0 < k; c0 += C) {
-        const int nt = min(C, k - c0);
+    // sources of chunk ch this wave moves: t = wave, wave + NW, ... < nt
+    auto own = [&](int ch) {
+        const int nt = min(C, k - ch * C);
+        return nt > wave ? (nt - wave + NW - 1) / NW : 0;
+    };
+    auto issue = [&](int ch) {
+        const int c0 = ch * C, nt = min(C, k - c0);
+        const uint32_t base = lds0 + (uint32_t)((ch & 1) * C * 2 * 64 * 16);
         for (int t = wave; t < nt; t += NW) {
-            uint32_t W[8];
-            load32(srcs[c0 + t], off, inb, W);
+            const uint8_t* row = sload_ptr(srcs + c0 + t) + loff;
+            glds16(row, base + (uint32_t)((t * 2 + 0) * 64 * 16));
+            glds16(row + 16, base + (uint32_t)((t * 2 + 1) * 64 * 16));
+        }
+    };
+
+    asm volatile(RSGPU_TC_ZERO ::: RSGPU_TC_ACC_CLOBBERS);
+
+    issue(0);
+    for (int ch = 0; ch < nch; ++ch) {
+        const int nt = min(C, k - ch * C);
+        uint4* buf = lds[ch & 1];
+        if (ch + 1 < nch) {
+            issue(ch + 1);  // lands while this chunk is transposed and consumed
+            wait_vm(2 * own(ch + 1));
+        } else {
+            wait_vm(0);
+        }
+        // own share of this chunk: bytes -> bit-planes, in place
+        for (int t = wave; t < nt; t += NW) {
+            uint4 u = buf[(t * 2 + 0) * 64 + lane];
+            uint4 v = buf[(t * 2 + 1) * 64 + lane];
+            uint32_t W[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
             tr8(W, m4, m2, m1);
-            lds[(t * 2 + 0) * 64 + lane] = make_uint4(W[0], W[1], W[2], W[3]);
-            lds[(t * 2 + 1) * 64 + lane] = make_uint4(W[4], W[5], W[6], W[7]);
+            buf[(t * 2 + 0) * 64 + lane] = make_uint4(W[0], W[1], W[2], W[3]);
+            buf[(t * 2 + 1) * 64 + lane] = make_uint4(W[4], W[5], W[6], W[7]);
         }
-        __syncthreads();
+        barrier_lds();
         for (int t = 0; t < nt; ++t) {
-            const uint4 u = lds[(t * 2 + 0) * 64 + lane];
-            const uint4 v = lds[(t * 2 + 1) * 64 + lane];
+            const uint4 u = buf[(t * 2 + 0) * 64 + lane];
+            const uint4 v = buf[(t * 2 + 1) * 64 + lane];
             const uint32_t P[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
-            const unsigned long long* pa = ap + (size_t)(c0 + t) * (NW * 8);
+            const unsigned long long* pa = ap + (size_t)(ch * C + t) * (NW * 8);
             asm volatile(RSGPU_TC_CONSUME
-                         : RSGPU_TC_ACC_OPS(acc)
+                         :
                          : RSGPU_TC_PLANE_OPS(P), [pa] "s"(pa)
-                         : RSGPU_TC_CLOBBERS);
+                         : RSGPU_TC_CLOBBERS, RSGPU_TC_ACC_CLOBBERS);
         }
-        __syncthreads();
+        barrier_lds();  // buffer ch & 1 is refilled by chunk ch + 2
     }
 
     if (!inb)
         return;
     uint8_t* const* dsts = a.dsts + (size_t)b * a.rows;
-#pragma unroll
-    for (int s = 0; s < 8; ++s) {
-        const int r = wave * 8 + s;
-        if (r < a.rows) {
-            uint32_t W[8];
-#pragma unroll
-            for (int q = 0; q < 8; ++q)
-                W[q] = acc[s * 8 + q];
-            tr8(W, m4, m2, m1);
-            store32(dsts[r], off, W);
-        }
-    }
+    [&]<int... Ss>(std::integer_sequence<int, Ss...>) {
+        (
+            [&] {
+                const int r = wave * 8 + Ss;
+                if (r < a.rows) {
+                    uint32_t W[8];
+                    read_slot<Ss>(W);
+                    tr8(W, m4, m2, m1);
+                    store32((uint8_t*)sload_ptr((const uint8_t* const*)(dsts + r)), off, W);
+                }
+            }(),
+            ...);
+    }(std::make_integer_sequence<int, 8>{});
 }
 
 }  // namespace tc
