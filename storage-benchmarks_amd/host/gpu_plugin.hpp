@@ -6,6 +6,7 @@
 
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <memory>
 #include <stdexcept>
 #include <string>
@@ -32,6 +33,26 @@ struct gpu_session {
 
 inline size_t row_pitch(uint32_t symbol_size) { return (symbol_size + 255u) / 256u * 256u; }
 
+// Process-wide session for the reference-shaped constructors (device from
+// RSGPU_DEVICE, default 0): throughput_benchmark.hpp:173-176 builds plugins
+// with (symbols, symbol_size, erased_symbols) only.
+inline std::shared_ptr<gpu_session> default_session()
+{
+    static std::shared_ptr<gpu_session> s = [] {
+        const char* d = std::getenv("RSGPU_DEVICE");
+        return std::make_shared<gpu_session>(d ? std::atoi(d) : 0);
+    }();
+    return s;
+}
+
+// Seed of the reference-shaped constructors (isa.cpp:55-58 uses rand(); the
+// erasure sets, isa.cpp:137-146, are drawn from the same seed here).
+inline uint64_t default_seed()
+{
+    const char* v = std::getenv("RSGPU_SEED");
+    return v ? std::strtoull(v, nullptr, 10) : 20240611ull;
+}
+
 struct gpu_encoder {
     gpu_encoder(std::shared_ptr<gpu_session> s, uint32_t symbols, uint32_t symbol_size,
                 uint32_t encoded_symbols, uint32_t blocks, uint64_t seed, uint64_t block0)
@@ -46,6 +67,15 @@ struct gpu_encoder {
                    "fill");
         m_s->check(rsgpu_synchronize(m_s->ctx), "sync");
     }
+    // Drop-in form of isa_encoder(symbols, symbol_size, encoded_symbols)
+    // (isa.cpp:31): one block, synchronous calls -- like the CPU library, the
+    // work is finished when encode_all() returns, so the reference harness's
+    // own timer measures it.
+    gpu_encoder(uint32_t symbols, uint32_t symbol_size, uint32_t encoded_symbols)
+        : gpu_encoder(default_session(), symbols, symbol_size, encoded_symbols, 1, default_seed(), 0)
+    {
+        synchronous = true;
+    }
     ~gpu_encoder()
     {
         rsgpu_free(m_s->ctx, src);
@@ -56,6 +86,8 @@ struct gpu_encoder {
     {
         m_s->check(rsgpu_encode_blocks(m_s->ctx, (int)k, (int)e, L, pitch, B, src, par, nullptr),
                    "rsgpu_encode_blocks");
+        if (synchronous)
+            finish();
     }
     void finish() { m_s->check(rsgpu_synchronize(m_s->ctx), "sync"); }
     uint32_t block_size() const { return k * L; }
@@ -69,6 +101,7 @@ struct gpu_encoder {
     size_t pitch;
     unsigned char* src = nullptr;
     unsigned char* par = nullptr;
+    bool synchronous = false;
 };
 
 struct gpu_decoder {
@@ -90,6 +123,13 @@ struct gpu_decoder {
         m_s->check(rsgpu_memcpy_h2d(m_s->ctx, err, h_err.data(), h_err.size()), "upload err");
         h_status.assign(B, -1);
     }
+    // Drop-in form of isa_decoder(symbols, symbol_size, erased_symbols)
+    // (isa.cpp:110): one block, synchronous, status fetched by decode_all.
+    gpu_decoder(uint32_t symbols, uint32_t symbol_size, uint32_t erased_symbols)
+        : gpu_decoder(default_session(), symbols, symbol_size, erased_symbols, 1, default_seed(), 0)
+    {
+        synchronous = true;
+    }
     ~gpu_decoder()
     {
         rsgpu_free(m_s->ctx, err);
@@ -105,6 +145,8 @@ struct gpu_decoder {
                                        err, out, ws, status),
                    "rsgpu_decode_blocks");
         m_decoded = true;
+        if (synchronous)
+            finish();
         return enc->payload_count();
     }
     void finish()
@@ -149,6 +191,7 @@ struct gpu_decoder {
     unsigned long long* mism = nullptr;
     std::vector<int> h_status;
     bool m_decoded = false;
+    bool synchronous = false;
 };
 
 }  // namespace sbamd

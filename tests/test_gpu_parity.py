@@ -257,3 +257,16 @@ def test_cpp_runner_end_to_end(tmp_path):
     assert len(lines) == 1 + 2 * 2 * 2  # symbols x type x runs
     for ln in lines[1:]:
         assert float(ln.split(",")[-1]) > 0
+
+
+@pytest.mark.gpu
+def test_plugin_dropin_reference_shape():
+    """gpu_encoder / gpu_decoder driven exactly as throughput_benchmark.hpp
+    drives isa_encoder / isa_decoder (3-argument constructors, synchronous
+    encode_all / decode_all, is_complete, verify_data)."""
+    import subprocess
+    exe = os.path.join(os.path.dirname(HERE), "storage-benchmarks_amd", "bin", "plugin_dropin_test")
+    r = subprocess.run([exe, "16:64000:8", "16:1000000:4", "64:1000000:32", "100:64000:20",
+                        "10:4096:4", "5:8192:4"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert r.stdout.count("complete=1 verified=1") == 6, r.stdout

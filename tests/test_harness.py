@@ -47,3 +47,12 @@ def test_cpp_runner_usage():
     assert r.returncode == 0 and "--symbols" in r.stdout
     r = subprocess.run([RUNNER, "--bogus"], capture_output=True, text=True)
     assert r.returncode == 2
+
+
+DROPIN = os.path.join(ROOT, "storage-benchmarks_amd", "bin", "plugin_dropin_test")
+
+
+@pytest.mark.skipif(not os.path.exists(DROPIN), reason="drop-in test not built")
+def test_dropin_rejects_bad_config_before_touching_the_gpu():
+    r = subprocess.run([DROPIN, "16-64000-8"], capture_output=True, text=True)
+    assert r.returncode == 2 and "symbols:symbol_size:erased" in r.stderr
