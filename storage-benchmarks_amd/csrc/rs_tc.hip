@@ -18,7 +18,10 @@
 //
 // Register contract (gen_tc_handlers.py): accumulators v[64:127] (8 slots x 8
 // planes), L/H tables v[32:61] with the source planes pinned at their
-// single-bit entries, handler addresses s[64:79], return address s[82:83].
+// single-bit entries, the next source's planes staged in v[24:31] and its
+// handler addresses in the other of two banks s[64:79] / s[84:99] while the
+// current source dispatches (one asm statement per LDS chunk, so every load
+// it starts is also waited for inside it), return address s[82:83].
 // The kernel therefore uses exactly 128 VGPRs: 4 waves per SIMD.
 //
 // Work split: as k_rs_bs -- a workgroup of NW waves covers 64 lanes x 32 bytes
@@ -27,6 +30,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+#include <cstdlib>
 #include <utility>
 
 #include "bitslice.h"
@@ -40,7 +45,7 @@ using bs::store32;
 using bs::tr8;
 using bs::vconst;
 
-constexpr int C = 8;  // sources per LDS chunk (double-buffered)
+constexpr int C = RSGPU_TC_C;  // sources per LDS chunk (double-buffered)
 
 // Holds the handler table; launched once per context to report where the
 // table sits (out[0] = first handler, out[1] = end of the table).  The
@@ -99,6 +104,35 @@ __device__ __forceinline__ const uint8_t* sload_ptr(const uint8_t* const* p)
     return r;
 }
 
+// Phase accounting for tools/tc_profile.hip (compiled in only there, with
+// -DRSGPU_TC_PROF): per-wave s_memtime sums of each phase, added into
+// rsgpu_tc_prof[phase] at the end of the wave.
+#ifdef RSGPU_TC_PROF
+__device__ unsigned long long rsgpu_tc_prof[8];
+#define TC_PROF_DECL unsigned long long tp_sum[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tp_t = __builtin_amdgcn_s_memtime(), tp_start = tp_t;
+#define TC_PROF_MARK(P)                                    \
+    do {                                                   \
+        const unsigned long long tp_n = __builtin_amdgcn_s_memtime(); \
+        tp_sum[P] += tp_n - tp_t;                          \
+        tp_t = tp_n;                                       \
+    } while (0)
+#define TC_PROF_END                                                                \
+    do {                                                                           \
+        tp_sum[7] = __builtin_amdgcn_s_memtime() - tp_start;                       \
+        if (lane == 0)                                                             \
+            for (int i = 0; i < 8; ++i)                                            \
+                atomicAdd(&rsgpu_tc_prof[i], tp_sum[i]);                           \
+    } while (0)
+#else
+#define TC_PROF_DECL
+#define TC_PROF_MARK(P) \
+    do {                \
+    } while (0)
+#define TC_PROF_END \
+    do {            \
+    } while (0)
+#endif
+
 // wait until at most N of this wave's vector-memory operations are pending
 __device__ __forceinline__ void wait_vm(int n)
 {
@@ -144,7 +178,7 @@ __device__ __forceinline__ void read_slot(uint32_t (&W)[8])
 // v64..v127 are touched by asm alone, so they stay put across the loops (the
 // kernel descriptor still reserves 128 VGPRs because the asm names v127).
 template <int NW>
-__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_num_vgpr(64))) void k_rs_tc(TcArgs a)
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_num_vgpr(64))) void k_rs_tc(TcArgs a, int tiles_per_wg)
 {
     // two chunk buffers [C][2 halves][64 lanes] of 16 bytes: 2 x 16 KiB
     __shared__ uint4 lds[2][C * 2 * 64];
@@ -153,12 +187,15 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_num_vgpr(64))) void 
     const int b = blockIdx.y;
     if (a.status && a.status[b] != 0)
         return;  // uniform per workgroup: the whole block is skipped
-    const long long off = (long long)blockIdx.x * 2048 + lane * 32;
-    const bool inb = off + 32 <= a.len;
-    const long long loff = inb ? off : 0;  // out-of-range lanes re-read the row head
+    // this workgroup's consecutive 2 KB column tiles of block b
+    const long long ntile = (a.len + 2047) / 2048;
+    const long long tile0 = (long long)blockIdx.x * tiles_per_wg;
+    const int my_tiles = (int)min((long long)tiles_per_wg, ntile - tile0);
     const int k = a.k;
     const int nch = (k + C - 1) / C;
+    const int total = my_tiles * nch;  // (tile, chunk) steps, pipelined across tiles
     const uint8_t* const* srcs = a.srcs + (size_t)b * k;
+    uint8_t* const* dsts = a.dsts + (size_t)b * a.rows;
     // addresses [B][k][NW*8]: this wave's 8 slots of source j at ap + j*NW*8
     const unsigned long long* ap = a.addr + (size_t)b * k * (NW * 8) + wave * 8;
     const uint32_t m4 = vconst(0x0F0F0F0Fu), m2 = vconst(0x33333333u), m1 = vconst(0x55555555u);
@@ -169,9 +206,12 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_num_vgpr(64))) void 
         const int nt = min(C, k - ch * C);
         return nt > wave ? (nt - wave + NW - 1) / NW : 0;
     };
-    auto issue = [&](int ch) {
+    auto issue = [&](int n) {
+        const int ch = n % nch;
+        const long long off = (tile0 + n / nch) * 2048 + lane * 32;
+        const long long loff = off + 32 <= a.len ? off : 0;  // out-of-range lanes re-read the row head
         const int c0 = ch * C, nt = min(C, k - c0);
-        const uint32_t base = lds0 + (uint32_t)((ch & 1) * C * 2 * 64 * 16);
+        const uint32_t base = lds0 + (uint32_t)((n & 1) * C * 2 * 64 * 16);
         for (int t = wave; t < nt; t += NW) {
             const uint8_t* row = sload_ptr(srcs + c0 + t) + loff;
             glds16(row, base + (uint32_t)((t * 2 + 0) * 64 * 16));
@@ -179,18 +219,21 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_num_vgpr(64))) void 
         }
     };
 
-    asm volatile(RSGPU_TC_ZERO ::: RSGPU_TC_ACC_CLOBBERS);
-
+    TC_PROF_DECL
     issue(0);
-    for (int ch = 0; ch < nch; ++ch) {
+    for (int n = 0; n < total; ++n) {
+        const int ch = n % nch;
         const int nt = min(C, k - ch * C);
-        uint4* buf = lds[ch & 1];
-        if (ch + 1 < nch) {
-            issue(ch + 1);  // lands while this chunk is transposed and consumed
-            wait_vm(2 * own(ch + 1));
+        uint4* buf = lds[n & 1];
+        TC_PROF_MARK(6);
+        if (n + 1 < total) {
+            issue(n + 1);  // lands while this chunk is transposed and consumed
+            TC_PROF_MARK(0);
+            wait_vm(2 * own((n + 1) % nch));
         } else {
             wait_vm(0);
         }
+        TC_PROF_MARK(1);
         // own share of this chunk: bytes -> bit-planes, in place
         for (int t = wave; t < nt; t += NW) {
             uint4 u = buf[(t * 2 + 0) * 64 + lane];
@@ -200,36 +243,60 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_num_vgpr(64))) void 
             buf[(t * 2 + 0) * 64 + lane] = make_uint4(W[0], W[1], W[2], W[3]);
             buf[(t * 2 + 1) * 64 + lane] = make_uint4(W[4], W[5], W[6], W[7]);
         }
+        TC_PROF_MARK(2);
         barrier_lds();
-        for (int t = 0; t < nt; ++t) {
-            const uint4 u = buf[(t * 2 + 0) * 64 + lane];
-            const uint4 v = buf[(t * 2 + 1) * 64 + lane];
-            const uint32_t P[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
-            const unsigned long long* pa = ap + (size_t)(ch * C + t) * (NW * 8);
-            asm volatile(RSGPU_TC_CONSUME
-                         :
-                         : RSGPU_TC_PLANE_OPS(P), [pa] "s"(pa)
-                         : RSGPU_TC_CLOBBERS, RSGPU_TC_ACC_CLOBBERS);
+        TC_PROF_MARK(3);
+        if (ch == 0)
+            asm volatile(RSGPU_TC_ZERO ::: RSGPU_TC_ACC_CLOBBERS);
+        // the chunk's nt sources: one asm statement (gen_tc_handlers.py)
+        {
+            const uint32_t la = lds0 + (uint32_t)((n & 1) * C * 2 * 64 * 16) + lane * 16;
+            const unsigned long long* pa = ap + (size_t)(ch * C) * (NW * 8);
+#define RSGPU_TC_RUN(N)                                                                          \
+    asm volatile(RSGPU_TC_CHUNK##N                                                               \
+                 :                                                                               \
+                 : [la] "v"(la), [pa] "s"(pa), [o1] "i"(1 * NW * 64), [o2] "i"(2 * NW * 64),      \
+                   [o3] "i"(3 * NW * 64), [o4] "i"(4 * NW * 64), [o5] "i"(5 * NW * 64),           \
+                   [o6] "i"(6 * NW * 64), [o7] "i"(7 * NW * 64)                                  \
+                 : RSGPU_TC_CLOBBERS, RSGPU_TC_ACC_CLOBBERS, "memory")
+            switch (nt) {
+            case 1: RSGPU_TC_RUN(1); break;
+            case 2: RSGPU_TC_RUN(2); break;
+            case 3: RSGPU_TC_RUN(3); break;
+            case 4: RSGPU_TC_RUN(4); break;
+            case 5: RSGPU_TC_RUN(5); break;
+            case 6: RSGPU_TC_RUN(6); break;
+            case 7: RSGPU_TC_RUN(7); break;
+            default: RSGPU_TC_RUN(8); break;
+            }
+#undef RSGPU_TC_RUN
         }
-        barrier_lds();  // buffer ch & 1 is refilled by chunk ch + 2
+        TC_PROF_MARK(4);
+        if (ch == nch - 1) {
+            // tile done: outputs back to bytes and out (all of this tile's
+            // sources were read before the previous barrier: in-place safe)
+            const long long off = (tile0 + n / nch) * 2048 + lane * 32;
+            if (off + 32 <= a.len) {
+                [&]<int... Ss>(std::integer_sequence<int, Ss...>) {
+                    (
+                        [&] {
+                            const int r = wave * 8 + Ss;
+                            if (r < a.rows) {
+                                uint32_t W[8];
+                                read_slot<Ss>(W);
+                                tr8(W, m4, m2, m1);
+                                store32((uint8_t*)sload_ptr((const uint8_t* const*)(dsts + r)), off, W);
+                            }
+                        }(),
+                        ...);
+                }(std::make_integer_sequence<int, 8>{});
+            }
+        }
+        TC_PROF_MARK(5);
+        barrier_lds();  // buffer n & 1 is refilled by step n + 2
     }
-
-    if (!inb)
-        return;
-    uint8_t* const* dsts = a.dsts + (size_t)b * a.rows;
-    [&]<int... Ss>(std::integer_sequence<int, Ss...>) {
-        (
-            [&] {
-                const int r = wave * 8 + Ss;
-                if (r < a.rows) {
-                    uint32_t W[8];
-                    read_slot<Ss>(W);
-                    tr8(W, m4, m2, m1);
-                    store32((uint8_t*)sload_ptr((const uint8_t* const*)(dsts + r)), off, W);
-                }
-            }(),
-            ...);
-    }(std::make_integer_sequence<int, 8>{});
+    TC_PROF_MARK(6);
+    TC_PROF_END;
 }
 
 }  // namespace tc
@@ -247,12 +314,20 @@ int tc_rows_per_pass(int rows) { return rows <= 0 ? 8 : (rows + 7) / 8 * 8; }
 hipError_t launch_rs_tc(const TcArgs& a, long long blocks, hipStream_t st)
 {
     const int nw = tc_rows_per_pass(a.rows) / 8;
-    dim3 grid((unsigned)((a.len + 2047) / 2048), (unsigned)blocks);
+    const long long ntile = (a.len + 2047) / 2048;
+    // consecutive tiles per workgroup: the LDS-DMA pipeline runs across tile
+    // boundaries, so only the first chunk of a workgroup waits on HBM cold
+    int tpw = 1;
+    if (const char* v = std::getenv("RSGPU_TC_TILES"))
+        tpw = std::max(1, std::atoi(v));
+    while (tpw > 1 && ntile * blocks / tpw < 2048)  // keep >= 2048 workgroups
+        tpw /= 2;
+    dim3 grid((unsigned)((ntile + tpw - 1) / tpw), (unsigned)blocks);
     switch (nw) {
-    case 1: hipLaunchKernelGGL(tc::k_rs_tc<1>, grid, dim3(64), 0, st, a); break;
-    case 2: hipLaunchKernelGGL(tc::k_rs_tc<2>, grid, dim3(128), 0, st, a); break;
-    case 3: hipLaunchKernelGGL(tc::k_rs_tc<3>, grid, dim3(192), 0, st, a); break;
-    case 4: hipLaunchKernelGGL(tc::k_rs_tc<4>, grid, dim3(256), 0, st, a); break;
+    case 1: hipLaunchKernelGGL(tc::k_rs_tc<1>, grid, dim3(64), 0, st, a, tpw); break;
+    case 2: hipLaunchKernelGGL(tc::k_rs_tc<2>, grid, dim3(128), 0, st, a, tpw); break;
+    case 3: hipLaunchKernelGGL(tc::k_rs_tc<3>, grid, dim3(192), 0, st, a, tpw); break;
+    case 4: hipLaunchKernelGGL(tc::k_rs_tc<4>, grid, dim3(256), 0, st, a, tpw); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
