@@ -83,5 +83,54 @@ __device__ __forceinline__ void store32(uint8_t* row, long long off, const uint3
     *(gv4u*)(row + off + 16) = b;
 }
 
+// 16 bytes per lane global -> LDS (LDS-DMA, no VGPR destination): lane i's
+// bytes land at lds_byte + 16 i.  M0 holds the LDS base and is restored.
+__device__ __forceinline__ void glds16(const void* g, uint32_t lds_byte)
+{
+    uint32_t keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n"
+        "s_mov_b32 m0, %2\n"
+        "s_nop 0\n"
+        "global_load_lds_dwordx4 %1, off\n"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(g), "s"(__builtin_amdgcn_readfirstlane(lds_byte))
+        : "memory");
+}
+
+// Wave-uniform pointer from a table through the scalar cache.  (hipcc would
+// use a vector load for it -- it cannot prove the table is not written -- and
+// its vmcnt(0) would drain the LDS-DMA in flight.)
+__device__ __forceinline__ const uint8_t* sload_ptr(const uint8_t* const* p)
+{
+    const uint8_t* r;
+    asm volatile("s_load_dwordx2 %0, %1, 0\n s_waitcnt lgkmcnt(0)" : "=s"(r) : "s"(p) : "memory");
+    return r;
+}
+
+// wait until at most N of this wave's vector-memory operations are pending
+__device__ __forceinline__ void wait_vm(int n)
+{
+    switch (n) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+    case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+    case 14: asm volatile("s_waitcnt vmcnt(14)" ::: "memory"); break;
+    case 16: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    }
+}
+
+// workgroup barrier that does not drain the LDS-DMA in flight
+__device__ __forceinline__ void barrier_lds()
+{
+    asm volatile("s_waitcnt lgkmcnt(0)\n s_barrier" ::: "memory");
+}
+
 }  // namespace bs
 }  // namespace rsgpu

@@ -178,28 +178,110 @@ struct Args {
     const uint64_t* emask;  // [B][2] erasure bitmask of the K originals (SYN only)
 };
 
-// One wave group: rows [R0, R0+NR).  LDS ring: [C][2][64] uint4 per chunk.
+// LDS part: S sources of [2 halves][64 lanes] x 16 B; two parts double-buffer
+// the source stream (2 x 16 KiB).  A plan chunk of C sources is ceil(C/S)
+// consecutive parts.
+constexpr int S = 8;
+
+// 64-bit wave-uniform copy (readfirstlane returns int: widen through
+// uint32_t, never sign-extend the low word)
+__device__ __forceinline__ uint64_t uniform64(uint64_t x)
+{
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)x);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(x >> 32));
+    return ((uint64_t)hi << 32) | lo;
+}
+
+template <int K, bool SYN>
+__device__ __forceinline__ bool is_live(int j, uint64_t em0, uint64_t em1)
+{
+    if (j >= K)
+        return false;
+    if constexpr (SYN)
+        return !(((j < 64 ? em0 >> j : em1 >> (j - 64)) & 1));
+    return true;
+}
+
+// Sources T = PART*S + t (t < S, T < C) of the current chunk from the LDS part.
+template <class P, int K, int C, int R0, int NR, int PART, bool SYN>
+__device__ __forceinline__ void consume_part(uint32_t (&acc)[NR][8], const uint4* buf, int lane,
+                                             int j0, uint64_t em0, uint64_t em1)
+{
+    [&]<int... Ts>(std::integer_sequence<int, Ts...>) {
+        (
+            [&] {
+                constexpr int T = PART * S + Ts;
+                if constexpr (T < C) {
+                    if (is_live<K, SYN>(j0 + Ts, em0, em1)) {
+                        const uint4 u = buf[(Ts * 2 + 0) * 64 + lane];
+                        const uint4 v = buf[(Ts * 2 + 1) * 64 + lane];
+                        const uint32_t pl[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
+                        consume<P, R0, NR, T>(acc, pl);
+                    }
+                    // keep the next source's LDS reads from being hoisted
+                    // here (they would pin 8 more VGPRs per source)
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            }(),
+            ...);
+    }(std::make_integer_sequence<int, S>{});
+}
+
+// One wave group: rows [R0, R0+NR).  The workgroup streams the sources
+// chunk by chunk (Horner order, last chunk first) through the LDS parts:
+// while part n is transposed in place and consumed, part n+1 is already in
+// flight by LDS-DMA (global_load_lds_dwordx4, counted vmcnt, raw barriers).
 template <int K, int E, int C, int NW, bool SYN, int G>
-__device__ __forceinline__ void run_group(const Args& a, uint4* lds)
+__device__ __forceinline__ void run_group(const Args& a, uint4 (*lds)[S * 2 * 64])
 {
     using P = PlanHolder<K, E, C>;
     constexpr int OPW = (E + NW - 1) / NW;
     constexpr int R0 = G * OPW;
     constexpr int NR = (E - R0) < OPW ? (E - R0) : OPW;
     constexpr int NCH = (K + C - 1) / C;
+    constexpr int NP = (C + S - 1) / S;  // parts per chunk
     static_assert(NR > 0, "empty wave group");
 
     const int lane = threadIdx.x & 63;
     const int b = blockIdx.y;
     const long long off = (long long)blockIdx.x * 2048 + lane * 32;
     const bool inb = off + 32 <= a.len;
+    const long long loff = inb ? off : 0;  // out-of-range lanes re-read the row head
     const uint8_t* sb = a.src + (size_t)b * K * a.pitch;
     uint64_t em0 = 0, em1 = 0;
-    if constexpr (SYN) {
-        em0 = a.emask[2 * b];
-        em1 = a.emask[2 * b + 1];
+    if constexpr (SYN) {  // wave-uniform: keep the masks (and every test of them) scalar
+        em0 = uniform64(a.emask[2 * b]);
+        em1 = uniform64(a.emask[2 * b + 1]);
     }
+    auto live = [&](int j) { return is_live<K, SYN>(j, em0, em1); };
     const uint32_t m4 = vconst(0x0F0F0F0Fu), m2 = vconst(0x33333333u), m1 = vconst(0x55555555u);
+    const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint4*)&lds[0][0];
+
+    // step n -> (chunk, part): chunks in Horner order NCH-1 .. 0
+    constexpr int NSTEP = NCH * NP;
+    auto first_src = [&](int n) { return (NCH - 1 - n / NP) * C + (n % NP) * S; };
+    auto part_len = [&](int n) {
+        const int p = n % NP;
+        return min(S, C - p * S);
+    };
+    // this wave's share of step n: t = G, G + NW, ... (live sources only)
+    auto issue = [&](int n) {
+        const int j0 = first_src(n), nt = part_len(n);
+        const uint32_t base = lds0 + (uint32_t)((n & 1) * S * 2 * 64 * 16);
+        for (int t = G; t < nt; t += NW)
+            if (live(j0 + t)) {
+                const uint8_t* row = sb + (size_t)(j0 + t) * a.pitch + loff;
+                bs::glds16(row, base + (uint32_t)((t * 2 + 0) * 64 * 16));
+                bs::glds16(row + 16, base + (uint32_t)((t * 2 + 1) * 64 * 16));
+            }
+    };
+    auto issued = [&](int n) {
+        const int j0 = first_src(n), nt = part_len(n);
+        int c = 0;
+        for (int t = G; t < nt; t += NW)
+            c += live(j0 + t) ? 2 : 0;
+        return c;
+    };
 
     uint32_t acc[NR][8];
 #pragma unroll
@@ -208,51 +290,36 @@ __device__ __forceinline__ void run_group(const Args& a, uint4* lds)
         for (int q = 0; q < 8; ++q)
             acc[r][q] = 0;
 
-    for (int ch = NCH - 1; ch >= 0; --ch) {
-        if constexpr (NW > 1) {
-            // load + transpose this wave's share of the chunk into LDS
-#pragma unroll
-            for (int t = G; t < C; t += NW) {
-                const int j = ch * C + t;
-                bool live = j < K;
-                if constexpr (SYN)
-                    live = live && !(((j < 64 ? em0 >> j : em1 >> (j - 64)) & 1));
-                uint32_t W[8];
-                load32(sb + (size_t)j * a.pitch, off, live && inb, W);
-                tr8(W, m4, m2, m1);
-                lds[(t * 2 + 0) * 64 + lane] = make_uint4(W[0], W[1], W[2], W[3]);
-                lds[(t * 2 + 1) * 64 + lane] = make_uint4(W[4], W[5], W[6], W[7]);
-            }
-            __syncthreads();
+    issue(0);
+    for (int n = 0; n < NSTEP; ++n) {
+        uint4* buf = lds[n & 1];
+        const int j0 = first_src(n), nt = part_len(n);
+        if (n + 1 < NSTEP) {
+            issue(n + 1);
+            bs::wait_vm(issued(n + 1));
+        } else {
+            bs::wait_vm(0);
         }
-        if (ch != NCH - 1)
+        for (int t = G; t < nt; t += NW)
+            if (live(j0 + t)) {
+                uint4 u = buf[(t * 2 + 0) * 64 + lane];
+                uint4 v = buf[(t * 2 + 1) * 64 + lane];
+                uint32_t W[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
+                tr8(W, m4, m2, m1);
+                buf[(t * 2 + 0) * 64 + lane] = make_uint4(W[0], W[1], W[2], W[3]);
+                buf[(t * 2 + 1) * 64 + lane] = make_uint4(W[4], W[5], W[6], W[7]);
+            }
+        bs::barrier_lds();
+        const int part = n % NP;
+        if (part == 0 && n != 0)
             twiddle_rows<P, R0, NR>(acc, std::make_integer_sequence<int, NR>{});
-        [&]<int... Ts>(std::integer_sequence<int, Ts...>) {
-            (
-                [&] {
-                    constexpr int T = Ts;
-                    const int j = ch * C + T;
-                    bool live = j < K;
-                    if constexpr (SYN)
-                        live = live && !(((j < 64 ? em0 >> j : em1 >> (j - 64)) & 1));
-                    if (live) {
-                        uint32_t p[8];
-                        if constexpr (NW > 1) {
-                            const uint4 u = lds[(T * 2 + 0) * 64 + lane];
-                            const uint4 v = lds[(T * 2 + 1) * 64 + lane];
-                            p[0] = u.x; p[1] = u.y; p[2] = u.z; p[3] = u.w;
-                            p[4] = v.x; p[5] = v.y; p[6] = v.z; p[7] = v.w;
-                        } else {
-                            load32(sb + (size_t)j * a.pitch, off, inb, p);
-                            tr8(p, m4, m2, m1);
-                        }
-                        consume<P, R0, NR, T>(acc, p);
-                    }
-                }(),
-                ...);
-        }(std::make_integer_sequence<int, C>{});
-        if constexpr (NW > 1)
-            __syncthreads();
+        // consume part `part` of the chunk: compile-time T = part*S + t
+        [&]<int... Ps>(std::integer_sequence<int, Ps...>) {
+            ((part == Ps ? consume_part<P, K, C, R0, NR, Ps, SYN>(acc, buf, lane, j0, em0, em1)
+                         : void()),
+             ...);
+        }(std::make_integer_sequence<int, NP>{});
+        bs::barrier_lds();  // part buffer n & 1 is refilled by step n + 2
     }
 
     if (!inb)
@@ -277,9 +344,9 @@ __device__ __forceinline__ void run_group(const Args& a, uint4* lds)
 }
 
 template <int K, int E, int C, int NW, bool SYN>
-__global__ __launch_bounds__(64 * NW, 4) void k_rs_bs(Args a)
+__global__ __launch_bounds__(64 * NW, 16 / NW) void k_rs_bs(Args a)  // 4 waves per SIMD
 {
-    __shared__ uint4 lds[NW > 1 ? C * 2 * 64 : 1];
+    __shared__ uint4 lds[2][S * 2 * 64];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     [&]<int... Gs>(std::integer_sequence<int, Gs...>) {
         ((wave == Gs ? run_group<K, E, C, NW, SYN, Gs>(a, lds) : void()), ...);

@@ -75,6 +75,7 @@ struct TcArgs {
     const uint8_t* const* srcs;      // [B][k]
     uint8_t* const* dsts;            // [B][rows]
     const unsigned long long* addr;  // [B][k][tc_rows_per_pass(rows)]
+    long long addr_stride;           // elements between blocks' tables (0: shared)
     int k, rows;
     long long len;
     const int* status;               // [B] or nullptr

@@ -41,7 +41,11 @@
 namespace rsgpu {
 namespace tc {
 
+using bs::barrier_lds;
+using bs::glds16;
+using bs::sload_ptr;
 using bs::store32;
+using bs::wait_vm;
 using bs::tr8;
 using bs::vconst;
 
@@ -78,32 +82,6 @@ __global__ void k_tc_handlers(unsigned long long* out)
     }
 }
 
-// 16 bytes per lane global -> LDS (LDS-DMA, no VGPR destination): lane i's
-// bytes land at lds_byte + 16 i.  M0 holds the LDS base and is restored.
-__device__ __forceinline__ void glds16(const void* g, uint32_t lds_byte)
-{
-    uint32_t keep;
-    asm volatile(
-        "s_mov_b32 %0, m0\n"
-        "s_mov_b32 m0, %2\n"
-        "s_nop 0\n"
-        "global_load_lds_dwordx4 %1, off\n"
-        "s_mov_b32 m0, %0"
-        : "=&s"(keep)
-        : "v"(g), "s"(lds_byte)
-        : "memory");
-}
-
-// Wave-uniform pointer from a table through the scalar cache.  (hipcc would
-// use a vector load for it -- it cannot prove the table is not written -- and
-// its vmcnt(0) would drain the LDS-DMA in flight.)
-__device__ __forceinline__ const uint8_t* sload_ptr(const uint8_t* const* p)
-{
-    const uint8_t* r;
-    asm volatile("s_load_dwordx2 %0, %1, 0\n s_waitcnt lgkmcnt(0)" : "=s"(r) : "s"(p) : "memory");
-    return r;
-}
-
 // Phase accounting for tools/tc_profile.hip (compiled in only there, with
 // -DRSGPU_TC_PROF): per-wave s_memtime sums of each phase, added into
 // rsgpu_tc_prof[phase] at the end of the wave.
@@ -119,7 +97,7 @@ __device__ unsigned long long rsgpu_tc_prof[8];
 #define TC_PROF_END                                                                \
     do {                                                                           \
         tp_sum[7] = __builtin_amdgcn_s_memtime() - tp_start;                       \
-        if (lane == 0)                                                             \
+        if (lane == 0 && (blockIdx.x & 63) == 0)  /* sampled: same-address atomics serialise */ \
             for (int i = 0; i < 8; ++i)                                            \
                 atomicAdd(&rsgpu_tc_prof[i], tp_sum[i]);                           \
     } while (0)
@@ -132,29 +110,6 @@ __device__ unsigned long long rsgpu_tc_prof[8];
     do {            \
     } while (0)
 #endif
-
-// wait until at most N of this wave's vector-memory operations are pending
-__device__ __forceinline__ void wait_vm(int n)
-{
-    switch (n) {
-    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
-    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
-    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
-    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
-    case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
-    case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
-    case 14: asm volatile("s_waitcnt vmcnt(14)" ::: "memory"); break;
-    case 16: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
-    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-    }
-}
-
-// workgroup barrier that does not drain the LDS-DMA in flight
-__device__ __forceinline__ void barrier_lds()
-{
-    asm volatile("s_waitcnt lgkmcnt(0)\n s_barrier" ::: "memory");
-}
 
 // Read accumulator slot S (asm-owned v[64+8S : 64+8S+7]) into W.
 template <int S>
@@ -197,7 +152,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_num_vgpr(64))) void 
     const uint8_t* const* srcs = a.srcs + (size_t)b * k;
     uint8_t* const* dsts = a.dsts + (size_t)b * a.rows;
     // addresses [B][k][NW*8]: this wave's 8 slots of source j at ap + j*NW*8
-    const unsigned long long* ap = a.addr + (size_t)b * k * (NW * 8) + wave * 8;
+    const unsigned long long* ap = a.addr + (size_t)b * a.addr_stride + wave * 8;
     const uint32_t m4 = vconst(0x0F0F0F0Fu), m2 = vconst(0x33333333u), m1 = vconst(0x55555555u);
     const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint4*)&lds[0][0];
 

@@ -27,6 +27,7 @@ struct rsgpu_ctx {
     // threaded-code solve (rs_tc.hip): device table of the 256 handler
     // addresses; tc_state 0 = not probed, 1 = ready, -1 = unavailable
     unsigned long long* d_tc_table = nullptr;
+    unsigned long long h_tc_table[256] = {};
     int tc_state = 0;
     std::string err;
     // grow-only device scratch for pointer tables / coefficient tables
@@ -47,6 +48,8 @@ struct rsgpu_ctx {
     std::vector<Rec> recs;
     std::vector<hipEvent_t> ev_pool;
 };
+
+static bool use_tc(rsgpu_ctx* ctx, int e);
 
 namespace {
 
@@ -191,6 +194,20 @@ struct KTimer {
         ctx->recs.push_back(rec);
     }
 };
+
+size_t tc_table_bytes(int k, int rows);
+void tc_fill_addr(const rsgpu_ctx* ctx, const uint8_t* coef, int k, int rows, unsigned long long* h);
+int tc_launch_shared(rsgpu_ctx* ctx, const unsigned long long* d_addr, int k, int rows, long long len,
+                     long long blocks, const uint8_t* const* d_srcs, uint8_t* const* d_dsts,
+                     const char* timer_name);
+
+// Runtime-coefficient dot product through the threaded-code kernel: host
+// coefficients coef[rows][k] become one handler-address table [k][slots]
+// shared by every block (uploaded to scratch at tab_off); rows <= 32, len %
+// 32 == 0, 16-byte aligned rows behind the device pointer tables.
+int tc_from_host_coef(rsgpu_ctx* ctx, const uint8_t* coef, int k, int rows, long long len,
+                      long long blocks, const uint8_t* const* d_srcs, uint8_t* const* d_dsts,
+                      size_t tab_off, const char* timer_name);
 
 // Fill host tables [k][rows_pad] for coefficient matrix coef[rows][k]
 // (coef row r column j at coef[r*k + j]).
@@ -509,7 +526,9 @@ int rsgpu_ec_encode_data(rsgpu_ctx* ctx, int len, int k, int rows, const unsigne
         aligned &= ((uintptr_t)coding[r] & 15) == 0;
     const size_t ptr_bytes = align_up(sizeof(void*) * (size_t)(k + rows), 256);
     const int rows_pad = rows_pad_for(rows);
-    const size_t tab_bytes = (size_t)k * rows_pad * (sizeof(uint4) + sizeof(uint32_t));
+    const bool tcp = aligned && len % 32 == 0 && use_tc(ctx, rows);
+    const size_t tab_bytes = tcp ? tc_table_bytes(k, rows)
+                                 : (size_t)k * rows_pad * (sizeof(uint4) + sizeof(uint32_t));
     int rc = ensure_scratch(ctx, ptr_bytes + tab_bytes);
     if (rc)
         return rc;
@@ -524,6 +543,17 @@ int rsgpu_ec_encode_data(rsgpu_ctx* ctx, int len, int k, int rows, const unsigne
         hp[j] = data[j];
     for (int r = 0; r < rows; ++r)
         hp[k + r] = coding[r];
+    if (tcp) {
+        // bit-sliced threaded-code kernel (rs_tc.hip): any coefficient matrix
+        tc_fill_addr(ctx, coef.data(), k, rows, (unsigned long long*)((char*)stage + ptr_bytes));
+        rc = upload(ctx, ctx->d_scratch, ptr_bytes + tab_bytes);
+        if (rc)
+            return rc;
+        char* d = (char*)ctx->d_scratch;
+        return tc_launch_shared(ctx, (const unsigned long long*)(d + ptr_bytes), k, rows, len, 1,
+                                (const uint8_t* const*)d, (uint8_t* const*)(d + sizeof(void*) * k),
+                                "k_rs_tc(ec_encode_data)");
+    }
     uint4* t4 = (uint4*)((char*)stage + ptr_bytes);
     uint32_t* tc = (uint32_t*)((char*)t4 + (size_t)k * rows_pad * sizeof(uint4));
     fill_tables(coef.data(), k, rows, rows_pad, t4, tc);
@@ -635,7 +665,8 @@ int rsgpu_encode_blocks(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch, 
     const size_t src_ptr_bytes = align_up(sizeof(void*) * (size_t)k * blocks, 256);
     const size_t dst_ptr_bytes = align_up(sizeof(void*) * (size_t)e * blocks, 256);
     const int rows_pad = rows_pad_for(e);
-    const size_t tab_bytes = (size_t)k * rows_pad * (sizeof(uint4) + sizeof(uint32_t));
+    const size_t tab_bytes = std::max((size_t)k * rows_pad * (sizeof(uint4) + sizeof(uint32_t)),
+                                      tc_table_bytes(k, e));
     rc = ensure_scratch(ctx, src_ptr_bytes + dst_ptr_bytes + tab_bytes);
     if (rc)
         return rc;
@@ -644,6 +675,10 @@ int rsgpu_encode_blocks(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch, 
                                 (const uint8_t**)d, ctx->stream));
     RS_HIP(ctx, launch_row_ptrs(d_parity, (long long)pitch, e, (long long)blocks,
                                 (const uint8_t**)(d + src_ptr_bytes), ctx->stream));
+    if (aligned && len % 32 == 0 && use_tc(ctx, e))
+        return tc_from_host_coef(ctx, c.data(), k, e, (long long)len, (long long)blocks,
+                                 (const uint8_t* const*)d, (uint8_t* const*)(d + src_ptr_bytes),
+                                 src_ptr_bytes + dst_ptr_bytes, "k_rs_tc(encode)");
     return generic_from_host_coef(ctx, c.data(), k, e, (long long)len, (long long)blocks,
                                   (const uint8_t* const*)d, (uint8_t* const*)(d + src_ptr_bytes),
                                   src_ptr_bytes + dst_ptr_bytes, !aligned);
@@ -682,10 +717,64 @@ static int tc_init(rsgpu_ctx* ctx)
         (void)hipFree(d);
         return -1;
     }
+    std::memcpy(ctx->h_tc_table, h, sizeof h);
     ctx->d_tc_table = d;
     ctx->tc_state = 1;
     return 1;
 }
+
+namespace {
+
+size_t tc_table_bytes(int k, int rows)
+{
+    return sizeof(unsigned long long) * (size_t)k * tc_rows_per_pass(rows);
+}
+
+void tc_fill_addr(const rsgpu_ctx* ctx, const uint8_t* coef, int k, int rows, unsigned long long* h)
+{
+    const int slots = tc_rows_per_pass(rows);
+    for (int j = 0; j < k; ++j)
+        for (int s = 0; s < slots; ++s)
+            h[(size_t)j * slots + s] = ctx->h_tc_table[s < rows ? coef[(size_t)s * k + j] : 0];
+}
+
+int tc_launch_shared(rsgpu_ctx* ctx, const unsigned long long* d_addr, int k, int rows, long long len,
+                     long long blocks, const uint8_t* const* d_srcs, uint8_t* const* d_dsts,
+                     const char* timer_name)
+{
+    TcArgs t{};
+    t.srcs = d_srcs;
+    t.dsts = d_dsts;
+    t.addr = d_addr;
+    t.addr_stride = 0;
+    t.k = k;
+    t.rows = rows;
+    t.len = len;
+    t.status = nullptr;
+    KTimer kt(ctx, timer_name, (size_t)blocks);
+    RS_HIP(ctx, launch_rs_tc(t, blocks, ctx->stream));
+    return RSGPU_OK;
+}
+
+int tc_from_host_coef(rsgpu_ctx* ctx, const uint8_t* coef, int k, int rows, long long len,
+                      long long blocks, const uint8_t* const* d_srcs, uint8_t* const* d_dsts,
+                      size_t tab_off, const char* timer_name)
+{
+    const size_t bytes = tc_table_bytes(k, rows);
+    void* stage;
+    int rc = get_stage(ctx, bytes, &stage);
+    if (rc)
+        return rc;
+    tc_fill_addr(ctx, coef, k, rows, (unsigned long long*)stage);
+    char* d = (char*)ctx->d_scratch + tab_off;
+    rc = upload(ctx, d, bytes);
+    if (rc)
+        return rc;
+    return tc_launch_shared(ctx, (const unsigned long long*)d, k, rows, len, blocks, d_srcs, d_dsts,
+                            timer_name);
+}
+
+}  // namespace
 
 // The threaded-code solve serves e <= 32 on the syndrome path.  Decided once
 // per context (RSGPU_NO_TC=1 at first use selects k_dot_generic instead, for
@@ -841,6 +930,7 @@ int rsgpu_decode_apply(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch, s
                 t.srcs = (const uint8_t* const*)(ws + o_surv) + b0 * e;
                 t.dsts = (uint8_t* const*)(ws + o_out) + b0 * e;
                 t.addr = (const unsigned long long*)(ws + o_tca) + b0 * e * tc_rows_per_pass(e);
+                t.addr_stride = (long long)e * tc_rows_per_pass(e);
                 t.k = e;
                 t.rows = e;
                 t.len = (long long)len;

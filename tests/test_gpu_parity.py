@@ -270,3 +270,72 @@ def test_plugin_dropin_reference_shape():
                         "10:4096:4", "5:8192:4"], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert r.stdout.count("complete=1 verified=1") == 6, r.stdout
+
+
+@pytest.mark.parametrize("k,e,L,B,kind", [
+    (32, 8, 4096, 3, "all256"),   # coefficient (r*32 + j) & 255: every value 0..255 once
+    (13, 20, 2048, 2, "random"),  # partial LDS chunks (13 = 8 + 5), 3 wave groups
+    (40, 32, 8192, 2, "random"),  # 5 chunks, 4 wave groups
+    (3, 1, 64, 1, "random"),      # smallest shapes
+])
+def test_runtime_coefficient_encode_tc(ctx, orc, k, e, L, B, kind):
+    """Arbitrary coefficient matrices through the threaded-code kernel
+    (k_rs_tc: len % 32 == 0, aligned rows) == the oracle's ec_encode_data_base."""
+    rng = np.random.default_rng(k * 1000 + e)
+    if kind == "all256":
+        coef = ((np.arange(e)[:, None] * k + np.arange(k)[None, :]) & 255).astype(np.uint8)
+    else:
+        coef = rng.integers(0, 256, (e, k), dtype=np.uint8)
+    enc = rsgpu.GpuEncoder(k, L, e, blocks=B, seed=9, ctx=ctx)
+    ctx.encode_blocks(k, e, L, enc.pitch, B, enc.src, enc.par, coef=coef)
+    torch.cuda.synchronize()
+    g = orc.init_tables(k, e, coef)
+    for blk in range(B):
+        data = list(enc.source_rows(blk))
+        ref = [np.zeros(L, np.uint8) for _ in range(e)]
+        orc.encode_data(L, k, e, g, data, ref)
+        got = enc.parity_rows(blk)
+        for p in range(e):
+            assert (got[p] == ref[p]).all(), (blk, p)
+
+
+def test_ec_encode_data_pointer_api_tc(ctx, orc):
+    """rsgpu_ec_encode_data with 32-multiple lengths and aligned rows takes the
+    threaded-code kernel; same bytes as ec_encode_data_base."""
+    rng = np.random.default_rng(77)
+    k, rows, length = 17, 11, 32 * 1001
+    coef = rng.integers(0, 256, (rows, k), dtype=np.uint8)
+    g = orc.init_tables(k, rows, coef)
+    data = [rng.integers(0, 256, length, dtype=np.uint8) for _ in range(k)]
+    d_data = [dev(d) for d in data]
+    d_out = [torch.zeros(length, dtype=torch.uint8, device="cuda") for _ in range(rows)]
+    ctx.timing_read()
+    ctx.timing_enable(True)
+    ctx.ec_encode_data(length, k, rows, g, d_data, d_out)
+    names = [n for n, _, _ in ctx.timing_read()]
+    ctx.timing_enable(False)
+    assert names == ["k_rs_tc(ec_encode_data)"], names
+    ref = [np.zeros(length, np.uint8) for _ in range(rows)]
+    orc.encode_data(length, k, rows, g, data, ref)
+    for r in range(rows):
+        assert (d_out[r].cpu().numpy() == ref[r]).all()
+
+
+@pytest.mark.parametrize("k,e,pattern", [
+    (64, 32, list(range(32))),                # bit 31 set, sources 32..63 all live
+    (64, 32, list(range(1, 64, 2))),          # odd sources: bits 31 and 63 set
+    (100, 20, [31, 63] + list(range(64, 82))),  # both 32-bit halves' sign bits + em1
+    (100, 20, list(range(80, 100))),          # only the high mask word
+])
+def test_syndrome_decode_sign_bit_masks(ctx, k, e, pattern):
+    """Erasure masks whose 32-bit halves have the sign bit set (a mask
+    sign-extended when made wave-uniform marked every higher source erased)."""
+    L, B = 4096, 2
+    enc = rsgpu.GpuEncoder(k, L, e, blocks=B, seed=4, ctx=ctx)
+    enc.encode_all()
+    errs = np.array([pattern] * B, np.uint8)
+    dec = rsgpu.GpuDecoder(k, L, e, blocks=B, seed=4, ctx=ctx, erasures=errs)
+    dec.decode_all(enc)
+    torch.cuda.synchronize()
+    assert dec.is_complete()
+    assert dec.verify_data(enc)

@@ -73,7 +73,7 @@ int main(int argc, char** argv)
     (void)hipEventElapsedTime(&ms, e0, e1);
     unsigned long long prof[8];
     (void)hipMemcpyFromSymbol(prof, HIP_SYMBOL(tc::rsgpu_tc_prof), sizeof prof);
-    const double waves = (double)((L + 2047) / 2048) * B * (slots / 8);
+    const double waves = (double)(((L + 2047) / 2048 + 63) / 64) * B * (slots / 8);  // sampled WGs
     const char* names[8] = {"issue DMA", "wait vmcnt", "transpose in", "barrier 1",
                             "chunk asm", "store out", "barrier 2 + loop", "wave lifetime"};
     printf("k_rs_tc<%d>: B=%d k=%d L=%lld  %.3f ms  (%.1f GB/s alg)\n", slots / 8, B, k, L, ms,
