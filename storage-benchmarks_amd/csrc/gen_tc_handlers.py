@@ -18,7 +18,8 @@ v0..v63 with amdgpu_num_vgpr(64), so v64..v127 belong to the asm alone):
     address banks       s[64:79], s[84:99]; m0 save s80; staged planes v[24:31]
     (all of these are clobbers of the one asm statement per chunk)
 
-usage: gen_tc_handlers.py OUT.inc
+usage: gen_tc_handlers.py OUT.inc [SYN.inc]
+  SYN.inc: compile-time syndrome blocks of the fused decode (rs_decode_fused.hip)
 """
 import sys
 
@@ -121,8 +122,128 @@ def chunk(nt: int) -> list:
     return ins
 
 
+def gf_pow2(n: int) -> int:
+    v = 1
+    for _ in range(n % 255):
+        v = gf_mul(v, 2)
+    return v
+
+
+# Codes with a fused syndrome decode (rs_decode_fused.hip): (K, E, C) =
+# (sources, parity rows, Horner chunk) of the gf_gen_rs_matrix code; E <= 32.
+# C = 8 keeps the fused kernel's code (every wave group's blocks + the 256
+# handlers) inside the instruction cache: C = 16 at (64, 32) thrashed it.
+SYN_PLANS = [(16, 4, 8), (16, 8, 8), (64, 32, 8), (64, 16, 8), (100, 20, 8), (5, 4, 5),
+             (20, 7, 8)]
+
+
+def mac_lines(c: int, slot: int) -> list:
+    """acc slot `slot` ^= c * (current source) from the L/H tables."""
+    ins = []
+    for b in range(8):
+        m = mat_row(c, b)
+        lo, hi = m & 15, m >> 4
+        acc = ACC + 8 * slot + b
+        if lo and hi:
+            ins.append(f"v_bitop3_b32 v{acc}, v{acc}, v{L0 + lo}, v{H0 + hi} bitop3:0x96")
+        elif lo:
+            ins.append(f"v_xor_b32_e32 v{acc}, v{L0 + lo}, v{acc}")
+        elif hi:
+            ins.append(f"v_xor_b32_e32 v{acc}, v{H0 + hi}, v{acc}")
+    return ins
+
+
+def tables() -> list:
+    ins = []
+    for base in (L0, H0):
+        for n in range(1, 16):
+            low = n & -n
+            if n != low:
+                ins.append(f"v_xor_b32_e32 v{base + n}, v{base + (n ^ low)}, v{base + low}")
+    return ins
+
+
+def syn_block(K: int, E: int, g: int, t: int) -> list:
+    """Compile-time syndrome MAC: source at chunk position t into the slots of
+    wave group g (rows r = 8g + s < E), coefficient 2^(r t)."""
+    ins = tables()
+    for s in range(8):
+        r = 8 * g + s
+        if r < E:
+            ins += mac_lines(gf_pow2(r * t), s)
+    return ins
+
+
+def syn_twiddle(E: int, C: int, g: int) -> list:
+    """Horner step between chunks: slot s (row r) *= 2^(C r), via temps v32..v39."""
+    ins = []
+    for s in range(8):
+        r = 8 * g + s
+        if r >= E:
+            continue
+        c = gf_pow2(C * r)
+        for b in range(8):
+            srcs = [ACC + 8 * s + a for a in range(8) if (mat_row(c, b) >> a) & 1]
+            tmp = 32 + b
+            if len(srcs) == 1:
+                ins.append(f"v_mov_b32_e32 v{tmp}, v{srcs[0]}")
+                continue
+            if len(srcs) == 2:
+                ins.append(f"v_xor_b32_e32 v{tmp}, v{srcs[0]}, v{srcs[1]}")
+                rest = []
+            else:
+                ins.append(f"v_bitop3_b32 v{tmp}, v{srcs[0]}, v{srcs[1]}, v{srcs[2]} bitop3:0x96")
+                rest = srcs[3:]
+            while len(rest) >= 2:
+                ins.append(f"v_bitop3_b32 v{tmp}, v{tmp}, v{rest[0]}, v{rest[1]} bitop3:0x96")
+                rest = rest[2:]
+            if rest:
+                ins.append(f"v_xor_b32_e32 v{tmp}, v{tmp}, v{rest[0]}")
+        for b in range(8):
+            ins.append(f"v_mov_b32_e32 v{ACC + 8 * s + b}, v{32 + b}")
+    return ins
+
+
+def write_syn(path: str) -> None:
+    """C++ specializations SynBlock<K,E,G,T> / SynTwiddle<K,E,G> / XorSlot<S>
+    wrapping the generated asm (rs_decode_fused.hip declares the primaries)."""
+    out = ["// generated by gen_tc_handlers.py -- do not edit"]
+    tab = [r for r in list(range(L0 + 1, L0 + 16)) + list(range(H0 + 1, H0 + 16)) if r not in PLANE_REG]
+    clob = ", ".join([f'"v{r}"' for r in tab] + [f'"v{ACC + i}"' for i in range(64)])
+    plane_ops = ", ".join(f'"{{v{r}}}"(P[{a}])' for a, r in enumerate(PLANE_REG))
+    tw_clob = ", ".join([f'"v{r}"' for r in range(32, 40)] + [f'"v{ACC + i}"' for i in range(64)])
+
+    def asm_text(ins):
+        return " ".join(f'"{i}\\n"' for i in ins)
+
+    for K, E, C in SYN_PLANS:
+        for g in range((E + 7) // 8):
+            for t in range(C):
+                out.append(f"template <> struct SynBlock<{K}, {E}, {g}, {t}> {{")
+                out.append("    __device__ __forceinline__ static void run(const uint32_t (&P)[8])")
+                out.append(f"    {{ asm volatile({asm_text(syn_block(K, E, g, t))} :: {plane_ops} : {clob}); }}")
+                out.append("};")
+            tw = syn_twiddle(E, C, g)
+            out.append(f"template <> struct SynTwiddle<{K}, {E}, {g}> {{")
+            out.append("    __device__ __forceinline__ static void run()")
+            out.append(f"    {{ asm volatile({asm_text(tw)} ::: {tw_clob}); }}")
+            out.append("};")
+    for s in range(8):
+        ins = [f"v_xor_b32_e32 v{ACC + 8 * s + b}, %{b}, v{ACC + 8 * s + b}" for b in range(8)]
+        ops = ", ".join(f'"v"(W[{b}])' for b in range(8))
+        acc_clob = ", ".join(f'"v{ACC + 8 * s + b}"' for b in range(8))
+        out.append(f"template <> struct XorSlot<{s}> {{")
+        out.append("    __device__ __forceinline__ static void run(const uint32_t (&W)[8])")
+        out.append(f"    {{ asm volatile({asm_text(ins)} :: {ops} : {acc_clob}); }}")
+        out.append("};")
+    with open(path, "w") as f:
+        f.write("\n".join(out) + "\n")
+
+
 def main() -> None:
     out = sys.argv[1]
+    if len(sys.argv) > 2:
+        write_syn(sys.argv[2])
     lines = [
         "// generated by gen_tc_handlers.py -- do not edit",
         f"#define RSGPU_TC_STRIDE {STRIDE}",

@@ -1,0 +1,337 @@
+// rs_decode_fused.hip -- one-pass syndrome decode for the gf_gen_rs_matrix
+// codes: recovered data rows from the surviving data rows and the parity rows
+// of each block, with HBM traffic (k + e) * L per block (read k, write e).
+//
+// The two-kernel decode (k_rs_bs<SYN> writes the e syndrome rows to HBM,
+// k_rs_tc reads them back and overwrites them with the data) moves 2 e L
+// more bytes.  Here one workgroup does both for its 2 KB column tile:
+//
+//   phase 1  s = P ^ V_kept d_kept        compile-time coefficients 2^(r j)
+//            (the k_rs_bs syndrome: sources streamed by LDS-DMA, bit-
+//            transposed in LDS, Horner over chunks of C sources), plus the
+//            parity rows; the e syndrome rows are stored to this tile of the
+//            output rows in bit-plane form (they stay L2/MALL resident)
+//   phase 2  x = V_E^-1 s                 runtime coefficients, threaded code
+//            (k_rs_tc's chunk asm over the e syndrome rows read back by
+//            LDS-DMA -- already planes, so no input transposes), then the
+//            rows are transposed to bytes and overwrite the syndromes.
+//
+// Both phases keep the accumulators in asm-owned v64..v127 (the compiler is
+// capped at v0..v63, amdgpu_num_vgpr(64)): phase 1's compile-time MAC blocks
+// are generated asm too (gen_tc_handlers.py -> build/syn_blocks.inc).
+// Wave w owns rows 8w..8w+7; NW = ceil(e / 8) waves per workgroup.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <utility>
+
+#include "bitslice.h"
+#include "rs_kernels.h"
+#include "tc_handlers.inc"
+
+namespace rsgpu {
+namespace fused {
+
+template <int K, int E, int G, int T>
+struct SynBlock;
+template <int K, int E, int G>
+struct SynTwiddle;
+template <int S>
+struct XorSlot;
+#include "syn_blocks.inc"
+
+using bs::barrier_lds;
+using bs::glds16;
+using bs::load32;
+using bs::store32;
+using bs::tr8;
+using bs::vconst;
+using bs::wait_vm;
+
+constexpr int S = 8;  // sources per LDS part (two parts double-buffer the stream)
+static_assert(S == RSGPU_TC_C, "phase 2 chunk asm reads parts of RSGPU_TC_C sources");
+
+struct Args {
+    const uint8_t* src;                // [B][K] rows
+    const uint8_t* par;                // [B][E] rows
+    uint8_t* out;                      // [B][E] rows (syndromes, then the data)
+    long long pitch, len;
+    const uint64_t* emask;             // [B][2] erased originals
+    const unsigned long long* addr;    // [B][E][8 NW] handler addresses of V_E^-1
+    const int* status;                 // [B]
+};
+
+__device__ __forceinline__ uint64_t uniform64(uint64_t x)
+{
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)x);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(x >> 32));
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// Read accumulator slot SL (asm-owned v[64+8SL .. 64+8SL+7]) into W.
+template <int SL>
+__device__ __forceinline__ void read_slot(uint32_t (&W)[8])
+{
+#define RSGPU_RD(TEXT)                                                                          \
+    asm volatile(TEXT : "=v"(W[0]), "=v"(W[1]), "=v"(W[2]), "=v"(W[3]), "=v"(W[4]), "=v"(W[5]), \
+                        "=v"(W[6]), "=v"(W[7]))
+    if constexpr (SL == 0) RSGPU_RD(RSGPU_TC_READ_SLOT0);
+    if constexpr (SL == 1) RSGPU_RD(RSGPU_TC_READ_SLOT1);
+    if constexpr (SL == 2) RSGPU_RD(RSGPU_TC_READ_SLOT2);
+    if constexpr (SL == 3) RSGPU_RD(RSGPU_TC_READ_SLOT3);
+    if constexpr (SL == 4) RSGPU_RD(RSGPU_TC_READ_SLOT4);
+    if constexpr (SL == 5) RSGPU_RD(RSGPU_TC_READ_SLOT5);
+    if constexpr (SL == 6) RSGPU_RD(RSGPU_TC_READ_SLOT6);
+    if constexpr (SL == 7) RSGPU_RD(RSGPU_TC_READ_SLOT7);
+#undef RSGPU_RD
+}
+
+// SynBlock<K, E, g, T> for the runtime (wave-uniform) wave group g
+template <int K, int E, int T, int NW>
+__device__ __forceinline__ void syn_block(int g, const uint32_t (&P)[8])
+{
+    [&]<int... Gs>(std::integer_sequence<int, Gs...>) {
+        ((g == Gs ? SynBlock<K, E, Gs, T>::run(P) : void()), ...);
+    }(std::make_integer_sequence<int, NW>{});
+}
+
+template <int K, int E, int NW>
+__device__ __forceinline__ void syn_twiddle(int g)
+{
+    [&]<int... Gs>(std::integer_sequence<int, Gs...>) {
+        ((g == Gs ? SynTwiddle<K, E, Gs>::run() : void()), ...);
+    }(std::make_integer_sequence<int, NW>{});
+}
+
+template <int K, int C, int E, int NW, int PART>
+__device__ __forceinline__ void syn_part(int G, const uint4* buf, int lane, int j0, uint64_t em0,
+                                         uint64_t em1)
+{
+    [&]<int... Ts>(std::integer_sequence<int, Ts...>) {
+        (
+            [&] {
+                constexpr int T = PART * S + Ts;
+                if constexpr (T < C) {
+                    const int j = j0 + Ts;
+                    const bool live = j < K && !(((j < 64 ? em0 >> j : em1 >> (j - 64)) & 1));
+                    if (live) {
+                        const uint4 u = buf[(Ts * 2 + 0) * 64 + lane];
+                        const uint4 v = buf[(Ts * 2 + 1) * 64 + lane];
+                        const uint32_t P[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
+                        syn_block<K, E, T, NW>(G, P);
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            }(),
+            ...);
+    }(std::make_integer_sequence<int, S>{});
+}
+
+// The scaffolding is shared by every wave group (G runtime, wave-uniform):
+// only the generated MAC / twiddle blocks differ per group, which keeps the
+// executed code of all groups plus the 256 handlers inside the I-cache.
+template <int K, int E, int C, int NW>
+__device__ __forceinline__ void run_group(const Args& a, uint4 (*lds)[S * 2 * 64], int G)
+{
+    constexpr int NCH = (K + C - 1) / C;
+    constexpr int NP = (C + S - 1) / S;
+    constexpr int NSTEP = NCH * NP;
+    const int lane = threadIdx.x & 63;
+    const int b = blockIdx.y;
+    const long long off = (long long)blockIdx.x * 2048 + lane * 32;
+    const bool inb = off + 32 <= a.len;
+    const long long loff = inb ? off : 0;  // out-of-range lanes re-read the row head
+    const uint8_t* sb = a.src + (size_t)b * K * a.pitch;
+    uint8_t* ob = a.out + (size_t)b * E * a.pitch;
+    const uint64_t em0 = uniform64(a.emask[2 * b]), em1 = uniform64(a.emask[2 * b + 1]);
+    auto live = [&](int j) { return j < K && !(((j < 64 ? em0 >> j : em1 >> (j - 64)) & 1)); };
+    const uint32_t m4 = vconst(0x0F0F0F0Fu), m2 = vconst(0x33333333u), m1 = vconst(0x55555555u);
+    const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint4*)&lds[0][0];
+
+    // ---------------- phase 1: syndromes ----------------
+    auto first_src = [&](int n) { return (NCH - 1 - n / NP) * C + (n % NP) * S; };
+    auto part_len = [&](int n) { return min(S, C - (n % NP) * S); };
+    auto issue1 = [&](int n) {
+        const int j0 = first_src(n), nt = part_len(n);
+        const uint32_t base = lds0 + (uint32_t)((n & 1) * S * 2 * 64 * 16);
+        for (int t = G; t < nt; t += NW)
+            if (live(j0 + t)) {
+                const uint8_t* row = sb + (size_t)(j0 + t) * a.pitch + loff;
+                glds16(row, base + (uint32_t)((t * 2 + 0) * 64 * 16));
+                glds16(row + 16, base + (uint32_t)((t * 2 + 1) * 64 * 16));
+            }
+    };
+    auto issued1 = [&](int n) {
+        const int j0 = first_src(n), nt = part_len(n);
+        int c = 0;
+        for (int t = G; t < nt; t += NW)
+            c += live(j0 + t) ? 2 : 0;
+        return c;
+    };
+
+    asm volatile(RSGPU_TC_ZERO ::: RSGPU_TC_ACC_CLOBBERS);
+    issue1(0);
+    for (int n = 0; n < NSTEP; ++n) {
+        uint4* buf = lds[n & 1];
+        const int j0 = first_src(n), nt = part_len(n);
+        if (n + 1 < NSTEP) {
+            issue1(n + 1);
+            wait_vm(issued1(n + 1));
+        } else {
+            wait_vm(0);
+        }
+        for (int t = G; t < nt; t += NW)
+            if (live(j0 + t)) {
+                uint4 u = buf[(t * 2 + 0) * 64 + lane];
+                uint4 v = buf[(t * 2 + 1) * 64 + lane];
+                uint32_t W[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
+                tr8(W, m4, m2, m1);
+                buf[(t * 2 + 0) * 64 + lane] = make_uint4(W[0], W[1], W[2], W[3]);
+                buf[(t * 2 + 1) * 64 + lane] = make_uint4(W[4], W[5], W[6], W[7]);
+            }
+        barrier_lds();
+        const int part = n % NP;
+        if (part == 0 && n != 0)
+            syn_twiddle<K, E, NW>(G);
+        [&]<int... Ps>(std::integer_sequence<int, Ps...>) {
+            ((part == Ps ? syn_part<K, C, E, NW, Ps>(G, buf, lane, j0, em0, em1) : void()), ...);
+        }(std::make_integer_sequence<int, NP>{});
+        barrier_lds();
+    }
+
+    // + parity rows (bytes -> planes), then the syndromes out in plane form
+    [&]<int... Ss>(std::integer_sequence<int, Ss...>) {
+        (
+            [&] {
+                const int r = G * 8 + Ss;
+                if (r < E) {
+                    uint32_t W[8];
+                    load32(a.par + ((size_t)b * E + r) * a.pitch, loff, true, W);
+                    tr8(W, m4, m2, m1);
+                    XorSlot<Ss>::run(W);
+                    read_slot<Ss>(W);
+                    if (inb)
+                        store32(ob + (size_t)r * a.pitch, off, W);
+                }
+            }(),
+            ...);
+    }(std::make_integer_sequence<int, 8>{});
+    // every wave's syndrome stores complete before any wave reads them back
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    barrier_lds();
+
+    // ---------------- phase 2: x = V_E^-1 s (threaded code) ----------------
+    constexpr int NCH2 = (E + S - 1) / S;
+    const unsigned long long* ap = a.addr + (size_t)b * E * (NW * 8) + G * 8;
+    auto issue2 = [&](int ch) {
+        const int c0 = ch * S, nt = min(S, E - c0);
+        const uint32_t base = lds0 + (uint32_t)((ch & 1) * S * 2 * 64 * 16);
+        for (int t = G; t < nt; t += NW) {
+            const uint8_t* row = ob + (size_t)(c0 + t) * a.pitch + loff;
+            glds16(row, base + (uint32_t)((t * 2 + 0) * 64 * 16));
+            glds16(row + 16, base + (uint32_t)((t * 2 + 1) * 64 * 16));
+        }
+    };
+    auto own2 = [&](int ch) {
+        const int nt = min(S, E - ch * S);
+        return nt > G ? 2 * ((nt - G + NW - 1) / NW) : 0;
+    };
+    asm volatile(RSGPU_TC_ZERO ::: RSGPU_TC_ACC_CLOBBERS);
+    issue2(0);
+    for (int ch = 0; ch < NCH2; ++ch) {
+        const int nt = min(S, E - ch * S);
+        if (ch + 1 < NCH2) {
+            issue2(ch + 1);
+            wait_vm(own2(ch + 1));
+        } else {
+            wait_vm(0);
+        }
+        barrier_lds();  // every wave's part of this chunk has landed
+        const uint32_t la = lds0 + (uint32_t)((ch & 1) * S * 2 * 64 * 16) + lane * 16;
+        const unsigned long long* pa = ap + (size_t)(ch * S) * (NW * 8);
+#define RSGPU_TC_RUN(N)                                                                          \
+    asm volatile(RSGPU_TC_CHUNK##N                                                               \
+                 :                                                                               \
+                 : [la] "v"(la), [pa] "s"(pa), [o1] "i"(1 * NW * 64), [o2] "i"(2 * NW * 64),      \
+                   [o3] "i"(3 * NW * 64), [o4] "i"(4 * NW * 64), [o5] "i"(5 * NW * 64),           \
+                   [o6] "i"(6 * NW * 64), [o7] "i"(7 * NW * 64)                                  \
+                 : RSGPU_TC_CLOBBERS, RSGPU_TC_ACC_CLOBBERS, "memory")
+        switch (nt) {
+        case 1: RSGPU_TC_RUN(1); break;
+        case 2: RSGPU_TC_RUN(2); break;
+        case 3: RSGPU_TC_RUN(3); break;
+        case 4: RSGPU_TC_RUN(4); break;
+        case 5: RSGPU_TC_RUN(5); break;
+        case 6: RSGPU_TC_RUN(6); break;
+        case 7: RSGPU_TC_RUN(7); break;
+        default: RSGPU_TC_RUN(8); break;
+        }
+#undef RSGPU_TC_RUN
+        barrier_lds();  // buffer ch & 1 is refilled by chunk ch + 2
+    }
+
+    if (!inb)
+        return;
+    // all syndrome rows of this tile were read before the last barrier: the
+    // data may overwrite them
+    [&]<int... Ss>(std::integer_sequence<int, Ss...>) {
+        (
+            [&] {
+                const int r = G * 8 + Ss;
+                if (r < E) {
+                    uint32_t W[8];
+                    read_slot<Ss>(W);
+                    tr8(W, m4, m2, m1);
+                    store32(ob + (size_t)r * a.pitch, off, W);
+                }
+            }(),
+            ...);
+    }(std::make_integer_sequence<int, 8>{});
+}
+
+template <int K, int E, int C>
+__global__ __launch_bounds__(64 * ((E + 7) / 8)) __attribute__((amdgpu_num_vgpr(64))) void
+k_rs_decode_fused(Args a)
+{
+    constexpr int NW = (E + 7) / 8;
+    __shared__ uint4 lds[2][S * 2 * 64];
+    if (a.status[blockIdx.y] != 0)
+        return;  // singular or malformed: the whole block is skipped
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    run_group<K, E, C, NW>(a, lds, wave);
+}
+
+template <int K, int E, int C>
+hipError_t launch(const Args& a, long long blocks, hipStream_t st)
+{
+    dim3 grid((unsigned)((a.len + 2047) / 2048), (unsigned)blocks);
+    hipLaunchKernelGGL((k_rs_decode_fused<K, E, C>), grid, dim3(64 * ((E + 7) / 8)), 0, st, a);
+    return hipGetLastError();
+}
+
+}  // namespace fused
+
+bool rs_decode_fused_available(int k, int e)
+{
+    return (k == 16 && e == 4) || (k == 16 && e == 8) || (k == 64 && e == 32) ||
+           (k == 64 && e == 16) || (k == 100 && e == 20) || (k == 5 && e == 4) ||
+           (k == 20 && e == 7);
+}
+
+hipError_t launch_rs_decode_fused(int k, int e, const uint8_t* src, const uint8_t* par,
+                                  uint8_t* out, long long pitch, long long len, long long blocks,
+                                  const uint64_t* emask, const unsigned long long* addr,
+                                  const int* status, hipStream_t st)
+{
+    fused::Args a{src, par, out, pitch, len, emask, addr, status};
+    if (k == 16 && e == 4) return fused::launch<16, 4, 8>(a, blocks, st);
+    if (k == 16 && e == 8) return fused::launch<16, 8, 8>(a, blocks, st);
+    if (k == 64 && e == 32) return fused::launch<64, 32, 8>(a, blocks, st);
+    if (k == 64 && e == 16) return fused::launch<64, 16, 8>(a, blocks, st);
+    if (k == 100 && e == 20) return fused::launch<100, 20, 8>(a, blocks, st);
+    if (k == 5 && e == 4) return fused::launch<5, 4, 5>(a, blocks, st);
+    if (k == 20 && e == 7) return fused::launch<20, 7, 8>(a, blocks, st);
+    return hipErrorInvalidValue;
+}
+
+}  // namespace rsgpu

@@ -81,6 +81,16 @@ struct TcArgs {
     const int* status;               // [B] or nullptr
 };
 int tc_rows_per_pass(int rows);
+
+// One-pass syndrome decode (rs_decode_fused.hip) for the instantiated
+// gf_gen_rs_matrix codes: out[b] = data rows listed by the prepare kernel's
+// emask, from src (surviving data) and par; addr = k_rs_tc handler addresses
+// of V_E^-1 ([B][e][tc_rows_per_pass(e)]); blocks with status != 0 skipped.
+bool rs_decode_fused_available(int k, int e);
+hipError_t launch_rs_decode_fused(int k, int e, const uint8_t* src, const uint8_t* par,
+                                  uint8_t* out, long long pitch, long long len, long long blocks,
+                                  const uint64_t* emask, const unsigned long long* addr,
+                                  const int* status, hipStream_t st);
 int tc_handler_stride();
 hipError_t tc_query_handlers(unsigned long long* d_out, hipStream_t st);
 hipError_t launch_rs_tc(const TcArgs& a, long long blocks, hipStream_t st);

@@ -791,6 +791,17 @@ static bool use_tc(rsgpu_ctx* ctx, int e)
     return tc_init(ctx) == 1;
 }
 
+// The one-pass fused decode (RSGPU_NO_FUSED=1 selects the two-kernel
+// syndrome + solve path instead, for comparison).
+static bool use_fused(rsgpu_ctx*, int k, int e)
+{
+    static const bool off = [] {
+        const char* v = std::getenv("RSGPU_NO_FUSED");
+        return v && v[0] == '1';
+    }();
+    return !off && rs_decode_fused_available(k, e);
+}
+
 // Syndrome decode (bit-sliced syndromes + runtime e x e in place) applies to
 // the instantiated codes with 32-byte-multiple rows; otherwise the direct
 // k x k inversion + e x k dot product.
@@ -902,6 +913,16 @@ int rsgpu_decode_apply(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch, s
         // on two streams so that the syndromes of chunk i+1 overlap the solve
         // of chunk i.
         const bool tcp = use_tc(ctx, e);
+        if (tcp && use_fused(ctx, k, e)) {
+            // one pass: syndromes + solve per column tile (rs_decode_fused.hip)
+            KTimer kt(ctx, "k_rs_decode_fused", blocks);
+            RS_HIP(ctx, launch_rs_decode_fused(k, e, d_src, d_parity, d_out, (long long)pitch,
+                                               (long long)len, (long long)blocks,
+                                               (const uint64_t*)ws,
+                                               (const unsigned long long*)(ws + o_tca), d_status,
+                                               ctx->stream));
+            return RSGPU_OK;
+        }
         const size_t chunks = decode_chunk_count(ctx, blocks);
         hipStream_t solve_stream = ctx->stream;
         if (chunks > 1) {
