@@ -49,6 +49,35 @@ using bs::vconst;
 using bs::wait_vm;
 
 constexpr int S = 8;  // sources per LDS part (two parts double-buffer the stream)
+
+// Phase accounting for tools/fused_profile.hip (-DRSGPU_FUSED_PROF only):
+// per-wave s_memtime sums per phase, sampled WGs, added into
+// rsgpu_fused_prof[phase] at the end of the wave.
+#ifdef RSGPU_FUSED_PROF
+__device__ unsigned long long rsgpu_fused_prof[16];
+#define FP_DECL unsigned long long fp_sum[16] = {}, fp_t = __builtin_amdgcn_s_memtime(), fp_start = fp_t;
+#define FP_MARK(P)                                                      \
+    do {                                                                \
+        const unsigned long long fp_n = __builtin_amdgcn_s_memtime();   \
+        fp_sum[P] += fp_n - fp_t;                                       \
+        fp_t = fp_n;                                                    \
+    } while (0)
+#define FP_END                                                                  \
+    do {                                                                        \
+        fp_sum[15] = __builtin_amdgcn_s_memtime() - fp_start;                   \
+        if (lane == 0 && (blockIdx.x & 63) == 0)                                \
+            for (int i = 0; i < 16; ++i)                                        \
+                atomicAdd(&rsgpu_fused_prof[i], fp_sum[i]);                     \
+    } while (0)
+#else
+#define FP_DECL
+#define FP_MARK(P) \
+    do {           \
+    } while (0)
+#define FP_END \
+    do {       \
+    } while (0)
+#endif
 static_assert(S == RSGPU_TC_C, "phase 2 chunk asm reads parts of RSGPU_TC_C sources");
 
 struct Args {
@@ -169,17 +198,21 @@ __device__ __forceinline__ void run_group(const Args& a, uint4 (*lds)[S * 2 * 64
         return c;
     };
 
+    FP_DECL
     asm volatile(RSGPU_TC_ZERO ::: RSGPU_TC_ACC_CLOBBERS);
     issue1(0);
     for (int n = 0; n < NSTEP; ++n) {
         uint4* buf = lds[n & 1];
         const int j0 = first_src(n), nt = part_len(n);
+        FP_MARK(5);
         if (n + 1 < NSTEP) {
             issue1(n + 1);
+            FP_MARK(0);
             wait_vm(issued1(n + 1));
         } else {
             wait_vm(0);
         }
+        FP_MARK(1);
         for (int t = G; t < nt; t += NW)
             if (live(j0 + t)) {
                 uint4 u = buf[(t * 2 + 0) * 64 + lane];
@@ -189,15 +222,19 @@ __device__ __forceinline__ void run_group(const Args& a, uint4 (*lds)[S * 2 * 64
                 buf[(t * 2 + 0) * 64 + lane] = make_uint4(W[0], W[1], W[2], W[3]);
                 buf[(t * 2 + 1) * 64 + lane] = make_uint4(W[4], W[5], W[6], W[7]);
             }
+        FP_MARK(2);
         barrier_lds();
+        FP_MARK(3);
         const int part = n % NP;
         if (part == 0 && n != 0)
             syn_twiddle<K, E, NW>(G);
         [&]<int... Ps>(std::integer_sequence<int, Ps...>) {
             ((part == Ps ? syn_part<K, C, E, NW, Ps>(G, buf, lane, j0, em0, em1) : void()), ...);
         }(std::make_integer_sequence<int, NP>{});
+        FP_MARK(4);
         barrier_lds();
     }
+    FP_MARK(5);
 
     // + parity rows (bytes -> planes), then the syndromes out in plane form
     [&]<int... Ss>(std::integer_sequence<int, Ss...>) {
@@ -219,6 +256,7 @@ __device__ __forceinline__ void run_group(const Args& a, uint4 (*lds)[S * 2 * 64
     // every wave's syndrome stores complete before any wave reads them back
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     barrier_lds();
+    FP_MARK(6);
 
     // ---------------- phase 2: x = V_E^-1 s (threaded code) ----------------
     constexpr int NCH2 = (E + S - 1) / S;
@@ -240,13 +278,16 @@ __device__ __forceinline__ void run_group(const Args& a, uint4 (*lds)[S * 2 * 64
     issue2(0);
     for (int ch = 0; ch < NCH2; ++ch) {
         const int nt = min(S, E - ch * S);
+        FP_MARK(10);
         if (ch + 1 < NCH2) {
             issue2(ch + 1);
             wait_vm(own2(ch + 1));
         } else {
             wait_vm(0);
         }
+        FP_MARK(7);
         barrier_lds();  // every wave's part of this chunk has landed
+        FP_MARK(8);
         const uint32_t la = lds0 + (uint32_t)((ch & 1) * S * 2 * 64 * 16) + lane * 16;
         const unsigned long long* pa = ap + (size_t)(ch * S) * (NW * 8);
 #define RSGPU_TC_RUN(N)                                                                          \
@@ -267,11 +308,15 @@ __device__ __forceinline__ void run_group(const Args& a, uint4 (*lds)[S * 2 * 64
         default: RSGPU_TC_RUN(8); break;
         }
 #undef RSGPU_TC_RUN
+        FP_MARK(9);
         barrier_lds();  // buffer ch & 1 is refilled by chunk ch + 2
     }
+    FP_MARK(10);
 
-    if (!inb)
+    if (!inb) {
+        FP_END;
         return;
+    }
     // all syndrome rows of this tile were read before the last barrier: the
     // data may overwrite them
     [&]<int... Ss>(std::integer_sequence<int, Ss...>) {
@@ -287,6 +332,8 @@ __device__ __forceinline__ void run_group(const Args& a, uint4 (*lds)[S * 2 * 64
             }(),
             ...);
     }(std::make_integer_sequence<int, 8>{});
+    FP_MARK(11);
+    FP_END;
 }
 
 template <int K, int E, int C>

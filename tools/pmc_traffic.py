@@ -16,6 +16,8 @@ from collections import defaultdict
 def name_of(kernel: str) -> str:
     if "k_rs_bs<" in kernel:
         return "k_rs_bs(syndrome)" if kernel.split(">")[0].rstrip().endswith("true") else "k_rs_bs(encode)"
+    if "k_rs_decode_fused" in kernel:
+        return "k_rs_decode_fused"
     if "k_rs_tc" in kernel:
         return "k_rs_tc(solve)"
     if "k_dot_generic" in kernel:
