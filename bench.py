@@ -52,6 +52,8 @@ def parse():
     p.add_argument("--seed", type=int, default=1)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-threads", type=int, default=None)
+    p.add_argument("--no-ref-base", action="store_true",
+                   help="skip the (slow, ~10 s) reference scalar-C CPU sample")
     p.add_argument("--no-verify", action="store_true")
     p.add_argument("--host-io", type=int, default=0, metavar="BLOCKS",
                    help="also time the host-resident path (H2D + kernel + D2H) on BLOCKS blocks")
@@ -129,25 +131,38 @@ def dist_env():
     return rank, world, local
 
 
-def cpu_baseline(k, e, L, threads):
-    """ISA-L base C compiled from the reference (oracle/_ref, kind "reference")
-    or our restatement timed the same way (kind "port"), on a bounded sample:
-    `threads` workers x 1 block of the same geometry, encode + decode timed
-    exactly as isa.cpp's timed regions."""
+def cpu_baseline(k, e, L, threads, kernel=1, blocks_per_thread=None):
+    """CPU baseline on the GPU box's host cores, isa.cpp's timed regions
+    (encode = matrix + tables + data kernel; decode = k x k inversion + tables
+    + data kernel) over a bounded sample: `threads` workers x
+    `blocks_per_thread` blocks of the same geometry.  Matrices, tables and
+    inversion are the reference's ISA-L 2.13 C compiled from /root/reference
+    (oracle/_ref).  The data kernel is
+      kernel 1: our AVX2 restatement of ISA-L's asm path (oracle/
+                isal_avx2_port.c; the yasm sources cannot be assembled in this
+                image) -> kind "port";
+      kernel 0: the reference's scalar ec_encode_data_base -> kind "reference".
+    """
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib
     if not oracle_lib.have_reference():
         return None
     ref = oracle_lib.Reference()
-    r = ref.cpu_bench(k, e, L, threads, 1, 7)
-    out_bytes = 2.0 * e * L * threads
+    if kernel == 1 and not ref.have_avx2:
+        return {"error": "host CPU has no AVX2"}
+    bpt = blocks_per_thread or (4 if kernel == 1 else 1)
+    r = ref.cpu_bench(k, e, L, threads, bpt, 7, kernel)
+    out_bytes = 2.0 * e * L * threads * bpt
     t = r["max_thread_s"]
+    what = ("AVX2 restatement of ISA-L 2.13 gf_vect_dot_prod_avx2/ec_encode_data_avx2"
+            if kernel == 1 else "ISA-L 2.13 ec_encode_data_base (reference scalar C)")
     return {"value": out_bytes / t / 2 ** 30, "unit": "GiB/s", "cores": threads,
-            "kind": "reference",
-            "sample": f"{threads} threads x 1 block (k={k}, e={e}, L={L}) encode+decode, "
-                      f"ISA-L 2.13 ec_base.c scalar path (no yasm for the AVX2 asm), "
-                      f"{t:.1f} s per thread, failures={r['failures']}",
-            "encode_s": r["enc_s"] / threads, "decode_s": r["dec_s"] / threads}
+            "kind": "port" if kernel == 1 else "reference",
+            "sample": f"{threads} threads x {bpt} block(s) (k={k}, e={e}, L={L}) encode+decode, "
+                      f"{what}, reference matrices/inversion; {t:.1f} s per thread, "
+                      f"failures={r['failures']}",
+            "encode_s_per_block": r["enc_s"] / (threads * bpt),
+            "decode_s_per_block": r["dec_s"] / (threads * bpt)}
 
 
 def main():
@@ -273,7 +288,9 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = args.cpu_threads or min(16, os.cpu_count() or 1)
         try:
-            line["cpu_baseline"] = cpu_baseline(k, e, L, threads)
+            line["cpu_baseline"] = cpu_baseline(k, e, L, threads, kernel=1)
+            if not args.no_ref_base:
+                line["cpu_baseline_reference"] = cpu_baseline(k, e, L, threads, kernel=0)
         except Exception as ex:  # reported, never fatal for the GPU number
             line["cpu_baseline"] = {"error": str(ex)}
     if rank == 0:

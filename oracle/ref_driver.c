@@ -56,22 +56,63 @@ void ref_gf_vect_mul(int len, unsigned char *a, unsigned char *src, unsigned cha
     gf_vect_mul_base(len, a, src, dest);
 }
 
+/* The data kernel of the timed regions: the reference's scalar
+ * ec_encode_data_base, or the AVX2 restatement of its asm path
+ * (isal_avx2_port.c; CPU baseline only). */
+typedef void (*data_kernel_t)(int, int, int, unsigned char *, unsigned char **, unsigned char **);
+void port_ec_encode_data_avx2(int len, int k, int rows, unsigned char *g, unsigned char **data,
+                              unsigned char **coding);
+int port_have_avx2(void);
+
+static void encode_block_with(data_kernel_t kern, int k, int e, int len, unsigned char **data,
+                              unsigned char **parity);
+static int decode_block_with(data_kernel_t kern, int k, int e, int len,
+                             const unsigned char *err_list, unsigned char **data,
+                             unsigned char **parity, unsigned char **out);
+
 /* isa.cpp:69-79 */
 void ref_encode_block(int k, int e, int len, unsigned char **data, unsigned char **parity)
+{
+    encode_block_with(ec_encode_data_base, k, e, len, data, parity);
+}
+
+/* isa.cpp:169-213 (err_list ascending, as std::set iterates) */
+int ref_decode_block(int k, int e, int len, const unsigned char *err_list,
+                     unsigned char **data, unsigned char **parity, unsigned char **out)
+{
+    return decode_block_with(ec_encode_data_base, k, e, len, err_list, data, parity, out);
+}
+
+/* the AVX2 port through the same flow (tests pin it against the base C) */
+void ref_encode_block_avx2(int k, int e, int len, unsigned char **data, unsigned char **parity)
+{
+    encode_block_with(port_ec_encode_data_avx2, k, e, len, data, parity);
+}
+
+int ref_decode_block_avx2(int k, int e, int len, const unsigned char *err_list,
+                          unsigned char **data, unsigned char **parity, unsigned char **out)
+{
+    return decode_block_with(port_ec_encode_data_avx2, k, e, len, err_list, data, parity, out);
+}
+
+int ref_have_avx2(void) { return port_have_avx2(); }
+
+static void encode_block_with(data_kernel_t kern, int k, int e, int len, unsigned char **data,
+                              unsigned char **parity)
 {
     int m = k + e;
     unsigned char *a = malloc((size_t)m * k);
     unsigned char *g = malloc((size_t)32 * k * (e ? e : 1));
     gf_gen_rs_matrix(a, m, k);
     ec_init_tables(k, m - k, &a[k * k], g);
-    ec_encode_data_base(len, k, m - k, g, data, parity);
+    kern(len, k, m - k, g, data, parity);
     free(a);
     free(g);
 }
 
-/* isa.cpp:169-213 (err_list ascending, as std::set iterates) */
-int ref_decode_block(int k, int e, int len, const unsigned char *err_list,
-                     unsigned char **data, unsigned char **parity, unsigned char **out)
+static int decode_block_with(data_kernel_t kern, int k, int e, int len,
+                             const unsigned char *err_list, unsigned char **data,
+                             unsigned char **parity, unsigned char **out)
 {
     int m = k + e, rc = 0;
     unsigned char *a = malloc((size_t)m * k), *b = malloc((size_t)k * k);
@@ -96,7 +137,7 @@ int ref_decode_block(int k, int e, int len, const unsigned char *err_list,
             for (int j = 0; j < k; ++j)
                 c[k * i + j] = d[k * err_list[i] + j];
         ec_init_tables(k, e, c, g);
-        ec_encode_data_base(len, k, e, g, surv, out);
+        kern(len, k, e, g, surv, out);
     }
     free(a); free(b); free(d); free(c); free(g); free(in_err); free(surv);
     return rc;
@@ -119,6 +160,7 @@ static inline uint64_t mix64(uint64_t z)
 
 typedef struct {
     int k, e, len, blocks_per_thread, tid;
+    data_kernel_t kern;
     uint64_t seed;
     double enc_s, dec_s;
     int failures;
@@ -144,6 +186,13 @@ static void *worker(void *arg)
         par[i] = aligned_alloc(64, ((size_t)len + 63) / 64 * 64);
         out[i] = aligned_alloc(64, ((size_t)len + 63) / 64 * 64);
     }
+    /* outputs pre-touched outside the timed region, so the timed kernels do
+     * not pay first-touch page faults (the reference's posix_memalign'd
+     * parity buffers would; this favours the CPU baseline) */
+    for (int i = 0; i < e; ++i) {
+        memset(par[i], 0, (size_t)len);
+        memset(out[i], 0, (size_t)len);
+    }
     unsigned char err[256], in_err[256];
     for (int b = 0; b < j->blocks_per_thread; ++b) {
         uint64_t blk = (uint64_t)j->tid * 1000003ull + (uint64_t)b;
@@ -165,9 +214,9 @@ static void *worker(void *arg)
             if (in_err[i])
                 err[n++] = (unsigned char)i;
         double t0 = now_s();
-        ref_encode_block(k, e, len, data, par);
+        encode_block_with(j->kern, k, e, len, data, par);
         double t1 = now_s();
-        int rc = ref_decode_block(k, e, len, err, data, par, out);
+        int rc = decode_block_with(j->kern, k, e, len, err, data, par, out);
         double t2 = now_s();
         j->enc_s += t1 - t0;
         j->dec_s += t2 - t1;
@@ -189,12 +238,25 @@ static void *worker(void *arg)
     return NULL;
 }
 
-/* Runs `threads` workers, each encoding+decoding `blocks_per_thread` blocks.
- * Returns wall seconds of the whole run; *enc_s / *dec_s are the summed
- * per-block timed-region seconds, *max_thread_s the largest per-thread sum
- * of both; *failures counts unrecovered symbols. */
+/* Runs `threads` workers, each encoding+decoding `blocks_per_thread` blocks
+ * with data kernel `kernel` (0 = reference ec_encode_data_base, 1 = AVX2
+ * port).  Returns wall seconds of the whole run; *enc_s / *dec_s are the
+ * summed per-block timed-region seconds, *max_thread_s the largest
+ * per-thread sum of both; *failures counts unrecovered symbols. */
+double ref_cpu_bench_kernel(int k, int e, int len, int threads, int blocks_per_thread,
+                            uint64_t seed, int kernel, double *enc_s, double *dec_s,
+                            double *max_thread_s, int *failures);
+
 double ref_cpu_bench(int k, int e, int len, int threads, int blocks_per_thread, uint64_t seed,
                      double *enc_s, double *dec_s, double *max_thread_s, int *failures)
+{
+    return ref_cpu_bench_kernel(k, e, len, threads, blocks_per_thread, seed, 0, enc_s, dec_s,
+                                max_thread_s, failures);
+}
+
+double ref_cpu_bench_kernel(int k, int e, int len, int threads, int blocks_per_thread,
+                            uint64_t seed, int kernel, double *enc_s, double *dec_s,
+                            double *max_thread_s, int *failures)
 {
     job_t *jobs = calloc((size_t)threads, sizeof(job_t));
     pthread_t *th = calloc((size_t)threads, sizeof(pthread_t));
@@ -202,6 +264,7 @@ double ref_cpu_bench(int k, int e, int len, int threads, int blocks_per_thread, 
     for (int t = 0; t < threads; ++t) {
         jobs[t].k = k; jobs[t].e = e; jobs[t].len = len;
         jobs[t].blocks_per_thread = blocks_per_thread; jobs[t].tid = t; jobs[t].seed = seed;
+        jobs[t].kern = kernel == 1 ? port_ec_encode_data_avx2 : ec_encode_data_base;
         pthread_create(&th[t], NULL, worker, &jobs[t]);
     }
     double es = 0, ds = 0, mx = 0;

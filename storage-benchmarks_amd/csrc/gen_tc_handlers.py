@@ -133,6 +133,8 @@ def gf_pow2(n: int) -> int:
 # (sources, parity rows, Horner chunk) of the gf_gen_rs_matrix code; E <= 32.
 # C = 8 keeps the fused kernel's code (every wave group's blocks + the 256
 # handlers) inside the instruction cache: C = 16 at (64, 32) thrashed it.
+# C = 16 at (64, 32) measured 32.5-32.6 ms against 32.3-32.4 for C = 8 even
+# with shared scaffolding (half the twiddles do not pay for the larger code).
 SYN_PLANS = [(16, 4, 8), (16, 8, 8), (64, 32, 8), (64, 16, 8), (100, 20, 8), (5, 4, 5),
              (20, 7, 8)]
 
@@ -174,33 +176,66 @@ def syn_block(K: int, E: int, g: int, t: int) -> list:
     return ins
 
 
+def lin_inplace(c: int, slot: int) -> list:
+    """acc slot `slot` := c * acc (the 8x8 GF(2) matrix of c applied to the
+    planes in place).  Outputs are written straight into their own plane when
+    no later output still needs that plane's old value; otherwise the old
+    value is first saved in a temp (v32..v39).  Identity rows cost nothing."""
+    base = ACC + 8 * slot
+    need = {b: [a for a in range(8) if (mat_row(c, b) >> a) & 1] for b in range(8)}
+    todo = [b for b in range(8) if need[b] != [b]]
+    loc = {a: base + a for a in range(8)}
+    ins, tmp = [], 32
+
+    def xor_into(dst, srcs):
+        if dst in srcs:  # the old value of dst must be read by the first op
+            srcs = [dst] + [x for x in srcs if x != dst]
+        if len(srcs) == 1:
+            ins.append(f"v_mov_b32_e32 v{dst}, v{srcs[0]}")
+            return
+        if len(srcs) == 2:
+            ins.append(f"v_xor_b32_e32 v{dst}, v{srcs[0]}, v{srcs[1]}")
+            return
+        ins.append(f"v_bitop3_b32 v{dst}, v{srcs[0]}, v{srcs[1]}, v{srcs[2]} bitop3:0x96")
+        rest = srcs[3:]
+        while len(rest) >= 2:
+            ins.append(f"v_bitop3_b32 v{dst}, v{dst}, v{rest[0]}, v{rest[1]} bitop3:0x96")
+            rest = rest[2:]
+        if rest:
+            ins.append(f"v_xor_b32_e32 v{dst}, v{dst}, v{rest[0]}")
+
+    while todo:
+        free = [b for b in todo if all(b not in need[o] for o in todo if o != b)]
+        b = free[0] if free else todo[0]
+        if not free:  # every remaining output still needs in_b: keep a copy
+            ins.append(f"v_mov_b32_e32 v{tmp}, v{base + b}")
+            loc[b] = tmp
+            tmp += 1
+            assert tmp <= 40
+        xor_into(base + b, [loc[a] for a in need[b]])
+        todo.remove(b)
+    return ins
+
+
 def syn_twiddle(E: int, C: int, g: int) -> list:
-    """Horner step between chunks: slot s (row r) *= 2^(C r), via temps v32..v39."""
+    """Horner step between chunks: slot s (row r) *= 2^(C r)."""
     ins = []
     for s in range(8):
         r = 8 * g + s
-        if r >= E:
-            continue
-        c = gf_pow2(C * r)
-        for b in range(8):
-            srcs = [ACC + 8 * s + a for a in range(8) if (mat_row(c, b) >> a) & 1]
-            tmp = 32 + b
-            if len(srcs) == 1:
-                ins.append(f"v_mov_b32_e32 v{tmp}, v{srcs[0]}")
-                continue
-            if len(srcs) == 2:
-                ins.append(f"v_xor_b32_e32 v{tmp}, v{srcs[0]}, v{srcs[1]}")
-                rest = []
-            else:
-                ins.append(f"v_bitop3_b32 v{tmp}, v{srcs[0]}, v{srcs[1]}, v{srcs[2]} bitop3:0x96")
-                rest = srcs[3:]
-            while len(rest) >= 2:
-                ins.append(f"v_bitop3_b32 v{tmp}, v{tmp}, v{rest[0]}, v{rest[1]} bitop3:0x96")
-                rest = rest[2:]
-            if rest:
-                ins.append(f"v_xor_b32_e32 v{tmp}, v{tmp}, v{rest[0]}")
-        for b in range(8):
-            ins.append(f"v_mov_b32_e32 v{ACC + 8 * s + b}, v{32 + b}")
+        if r < E:
+            ins += lin_inplace(gf_pow2(C * r), s)
+    return ins
+
+
+def syn_prescale(K: int, E: int, C: int, g: int) -> list:
+    """Parity rows enter the accumulators before the first chunk, scaled by
+    2^(-C r (NCH-1)): the NCH-1 Horner twiddles bring them back to P_r."""
+    nch = (K + C - 1) // C
+    ins = []
+    for s in range(8):
+        r = 8 * g + s
+        if r < E:
+            ins += lin_inplace(gf_pow2((-C * r * (nch - 1)) % 255), s)
     return ins
 
 
@@ -216,18 +251,27 @@ def write_syn(path: str) -> None:
     def asm_text(ins):
         return " ".join(f'"{i}\\n"' for i in ins)
 
+    # MAC blocks depend on (K, E, g, t) only: one set per code, t < the
+    # largest chunk any plan of that code uses; twiddles depend on C too
+    tmax = {}
     for K, E, C in SYN_PLANS:
+        tmax[(K, E)] = max(tmax.get((K, E), 0), C)
+    for (K, E), CM in tmax.items():
         for g in range((E + 7) // 8):
-            for t in range(C):
+            for t in range(CM):
                 out.append(f"template <> struct SynBlock<{K}, {E}, {g}, {t}> {{")
                 out.append("    __device__ __forceinline__ static void run(const uint32_t (&P)[8])")
                 out.append(f"    {{ asm volatile({asm_text(syn_block(K, E, g, t))} :: {plane_ops} : {clob}); }}")
                 out.append("};")
-            tw = syn_twiddle(E, C, g)
-            out.append(f"template <> struct SynTwiddle<{K}, {E}, {g}> {{")
-            out.append("    __device__ __forceinline__ static void run()")
-            out.append(f"    {{ asm volatile({asm_text(tw)} ::: {tw_clob}); }}")
-            out.append("};")
+    for K, E, C in SYN_PLANS:
+        for g in range((E + 7) // 8):
+            for name, body in (("SynTwiddle", syn_twiddle(E, C, g)),
+                               ("SynPreScale", syn_prescale(K, E, C, g))):
+                out.append(f"template <> struct {name}<{K}, {E}, {C}, {g}> {{")
+                out.append("    __device__ __forceinline__ static void run()")
+                text = asm_text(body) if body else '""'
+                out.append(f"    {{ asm volatile({text} ::: {tw_clob}); }}")
+                out.append("};")
     for s in range(8):
         ins = [f"v_xor_b32_e32 v{ACC + 8 * s + b}, %{b}, v{ACC + 8 * s + b}" for b in range(8)]
         ops = ", ".join(f'"v"(W[{b}])' for b in range(8))
@@ -272,6 +316,13 @@ def main() -> None:
     for slot in range(8):
         body = "".join(f"v_mov_b32 %{q}, v{ACC + 8 * slot + q}\\n" for q in range(8))
         lines.append(f'#define RSGPU_TC_READ_SLOT{slot} "{body}"')
+    for slot in range(8):
+        body = "".join(f"v_mov_b32 v{ACC + 8 * slot + q}, %{q}\\n" for q in range(8))
+        lines.append(f'#define RSGPU_TC_WRITE_SLOT{slot} "{body}"')
+    for slot in range(8):
+        a0 = ACC + 8 * slot
+        lines.append(f'#define RSGPU_TC_LOAD_SLOT{slot} "global_load_dwordx4 v[{a0}:{a0 + 3}], %0, off\\n'
+                     f'global_load_dwordx4 v[{a0 + 4}:{a0 + 7}], %0, off offset:16\\n"')
     lines.append("#define RSGPU_TC_ACC_CLOBBERS " + ", ".join(f'"v{ACC + i}"' for i in range(64)))
     vclob = list(range(STAGE, STAGE + 8)) + list(range(L0 + 1, L0 + 16)) + list(range(H0 + 1, H0 + 16))
     sclob = list(range(BANK[0], BANK[0] + 16)) + [SM0, RET, RET + 1] + list(range(BANK[1], BANK[1] + 16))

@@ -343,8 +343,18 @@ __device__ __forceinline__ void run_group(const Args& a, uint4 (*lds)[S * 2 * 64
     }
 }
 
+// waves per SIMD the register budget must allow: 4 while a wave owns <= 8 rows
+// (64 accumulator VGPRs), 2 for 16 rows (128 accumulators; halves the
+// per-wave four-Russians table builds, but measured slower at (64, 32):
+// 24.2 vs 23.2 ms, two waves per SIMD do not hide the LDS-DMA pipeline)
+template <int E, int NW>
+constexpr int bs_waves_per_simd()
+{
+    return (E + NW - 1) / NW > 8 ? 2 : 16 / NW;
+}
+
 template <int K, int E, int C, int NW, bool SYN>
-__global__ __launch_bounds__(64 * NW, 16 / NW) void k_rs_bs(Args a)  // 4 waves per SIMD
+__global__ __launch_bounds__(64 * NW, (bs_waves_per_simd<E, NW>())) void k_rs_bs(Args a)
 {
     __shared__ uint4 lds[2][S * 2 * 64];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);

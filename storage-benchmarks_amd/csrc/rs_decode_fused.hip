@@ -8,9 +8,12 @@
 //
 //   phase 1  s = P ^ V_kept d_kept        compile-time coefficients 2^(r j)
 //            (the k_rs_bs syndrome: sources streamed by LDS-DMA, bit-
-//            transposed in LDS, Horner over chunks of C sources), plus the
-//            parity rows; the e syndrome rows are stored to this tile of the
-//            output rows in bit-plane form (they stay L2/MALL resident)
+//            transposed in LDS, Horner over chunks of C sources).  The
+//            parity rows are loaded into the accumulators first, scaled by
+//            2^(-C r (NCH-1)) so the Horner twiddles return them to P_r: their
+//            load overlaps the first LDS-DMA part instead of ending the phase.
+//            The e syndrome rows are stored to this tile of the output rows in
+//            bit-plane form (they stay L2/MALL resident)
 //   phase 2  x = V_E^-1 s                 runtime coefficients, threaded code
 //            (k_rs_tc's chunk asm over the e syndrome rows read back by
 //            LDS-DMA -- already planes, so no input transposes), then the
@@ -34,15 +37,16 @@ namespace fused {
 
 template <int K, int E, int G, int T>
 struct SynBlock;
-template <int K, int E, int G>
+template <int K, int E, int C, int G>
 struct SynTwiddle;
+template <int K, int E, int C, int G>
+struct SynPreScale;
 template <int S>
 struct XorSlot;
 #include "syn_blocks.inc"
 
 using bs::barrier_lds;
 using bs::glds16;
-using bs::load32;
 using bs::store32;
 using bs::tr8;
 using bs::vconst;
@@ -115,6 +119,41 @@ __device__ __forceinline__ void read_slot(uint32_t (&W)[8])
 #undef RSGPU_RD
 }
 
+// Write W into accumulator slot SL.
+template <int SL>
+__device__ __forceinline__ void write_slot(const uint32_t (&W)[8])
+{
+#define RSGPU_WR(TEXT)                                                                          \
+    asm volatile(TEXT ::"v"(W[0]), "v"(W[1]), "v"(W[2]), "v"(W[3]), "v"(W[4]), "v"(W[5]), \
+                 "v"(W[6]), "v"(W[7]))
+    if constexpr (SL == 0) RSGPU_WR(RSGPU_TC_WRITE_SLOT0);
+    if constexpr (SL == 1) RSGPU_WR(RSGPU_TC_WRITE_SLOT1);
+    if constexpr (SL == 2) RSGPU_WR(RSGPU_TC_WRITE_SLOT2);
+    if constexpr (SL == 3) RSGPU_WR(RSGPU_TC_WRITE_SLOT3);
+    if constexpr (SL == 4) RSGPU_WR(RSGPU_TC_WRITE_SLOT4);
+    if constexpr (SL == 5) RSGPU_WR(RSGPU_TC_WRITE_SLOT5);
+    if constexpr (SL == 6) RSGPU_WR(RSGPU_TC_WRITE_SLOT6);
+    if constexpr (SL == 7) RSGPU_WR(RSGPU_TC_WRITE_SLOT7);
+#undef RSGPU_WR
+}
+
+// Start loading 32 bytes per lane of `row` into accumulator slot SL (two
+// global_load_dwordx4, counted in vmcnt; the caller waits before reading it).
+template <int SL>
+__device__ __forceinline__ void load_slot(const uint8_t* row)
+{
+#define RSGPU_LD(TEXT) asm volatile(TEXT ::"v"(row) : "memory")
+    if constexpr (SL == 0) RSGPU_LD(RSGPU_TC_LOAD_SLOT0);
+    if constexpr (SL == 1) RSGPU_LD(RSGPU_TC_LOAD_SLOT1);
+    if constexpr (SL == 2) RSGPU_LD(RSGPU_TC_LOAD_SLOT2);
+    if constexpr (SL == 3) RSGPU_LD(RSGPU_TC_LOAD_SLOT3);
+    if constexpr (SL == 4) RSGPU_LD(RSGPU_TC_LOAD_SLOT4);
+    if constexpr (SL == 5) RSGPU_LD(RSGPU_TC_LOAD_SLOT5);
+    if constexpr (SL == 6) RSGPU_LD(RSGPU_TC_LOAD_SLOT6);
+    if constexpr (SL == 7) RSGPU_LD(RSGPU_TC_LOAD_SLOT7);
+#undef RSGPU_LD
+}
+
 // SynBlock<K, E, g, T> for the runtime (wave-uniform) wave group g
 template <int K, int E, int T, int NW>
 __device__ __forceinline__ void syn_block(int g, const uint32_t (&P)[8])
@@ -124,11 +163,19 @@ __device__ __forceinline__ void syn_block(int g, const uint32_t (&P)[8])
     }(std::make_integer_sequence<int, NW>{});
 }
 
-template <int K, int E, int NW>
+template <int K, int E, int C, int NW>
 __device__ __forceinline__ void syn_twiddle(int g)
 {
     [&]<int... Gs>(std::integer_sequence<int, Gs...>) {
-        ((g == Gs ? SynTwiddle<K, E, Gs>::run() : void()), ...);
+        ((g == Gs ? SynTwiddle<K, E, C, Gs>::run() : void()), ...);
+    }(std::make_integer_sequence<int, NW>{});
+}
+
+template <int K, int E, int C, int NW>
+__device__ __forceinline__ void syn_prescale(int g)
+{
+    [&]<int... Gs>(std::integer_sequence<int, Gs...>) {
+        ((g == Gs ? SynPreScale<K, E, C, Gs>::run() : void()), ...);
     }(std::make_integer_sequence<int, NW>{});
 }
 
@@ -200,7 +247,30 @@ __device__ __forceinline__ void run_group(const Args& a, uint4 (*lds)[S * 2 * 64
 
     FP_DECL
     asm volatile(RSGPU_TC_ZERO ::: RSGPU_TC_ACC_CLOBBERS);
+    // parity rows straight into this wave's accumulators; their latency
+    // overlaps the first LDS-DMA part
+    [&]<int... Ss>(std::integer_sequence<int, Ss...>) {
+        ((G * 8 + Ss < E ? load_slot<Ss>(a.par + ((size_t)b * E + G * 8 + Ss) * a.pitch + loff)
+                         : void()),
+         ...);
+    }(std::make_integer_sequence<int, 8>{});
     issue1(0);
+    wait_vm(issued1(0));  // the (older) parity loads have landed
+    // bytes -> planes, scaled by 2^(-C r (NCH-1)): the NCH-1 Horner twiddles
+    // of the chunk loop bring them back to P_r
+    [&]<int... Ss>(std::integer_sequence<int, Ss...>) {
+        (
+            [&] {
+                if (G * 8 + Ss < E) {
+                    uint32_t W[8];
+                    read_slot<Ss>(W);
+                    tr8(W, m4, m2, m1);
+                    write_slot<Ss>(W);
+                }
+            }(),
+            ...);
+    }(std::make_integer_sequence<int, 8>{});
+    syn_prescale<K, E, C, NW>(G);
     for (int n = 0; n < NSTEP; ++n) {
         uint4* buf = lds[n & 1];
         const int j0 = first_src(n), nt = part_len(n);
@@ -227,7 +297,7 @@ __device__ __forceinline__ void run_group(const Args& a, uint4 (*lds)[S * 2 * 64
         FP_MARK(3);
         const int part = n % NP;
         if (part == 0 && n != 0)
-            syn_twiddle<K, E, NW>(G);
+            syn_twiddle<K, E, C, NW>(G);
         [&]<int... Ps>(std::integer_sequence<int, Ps...>) {
             ((part == Ps ? syn_part<K, C, E, NW, Ps>(G, buf, lane, j0, em0, em1) : void()), ...);
         }(std::make_integer_sequence<int, NP>{});
@@ -236,26 +306,31 @@ __device__ __forceinline__ void run_group(const Args& a, uint4 (*lds)[S * 2 * 64
     }
     FP_MARK(5);
 
-    // + parity rows (bytes -> planes), then the syndromes out in plane form
+    // The syndromes (parity included), in plane form, are phase 2's sources:
+    // wave G's rows are its chunk G.  Waves 0 and 1 write theirs straight
+    // into the two LDS part buffers (both free after the last barrier);
+    // later waves park theirs in this tile of the output rows (L2 / MALL)
+    // and phase 2 fetches them back by LDS-DMA one chunk ahead.
+    constexpr int NLDS = 2;  // chunks handed over through LDS
     [&]<int... Ss>(std::integer_sequence<int, Ss...>) {
         (
             [&] {
                 const int r = G * 8 + Ss;
                 if (r < E) {
                     uint32_t W[8];
-                    load32(a.par + ((size_t)b * E + r) * a.pitch, loff, true, W);
-                    tr8(W, m4, m2, m1);
-                    XorSlot<Ss>::run(W);
                     read_slot<Ss>(W);
-                    if (inb)
+                    if (G < NLDS) {
+                        uint4* dst = lds[G];
+                        dst[(Ss * 2 + 0) * 64 + lane] = make_uint4(W[0], W[1], W[2], W[3]);
+                        dst[(Ss * 2 + 1) * 64 + lane] = make_uint4(W[4], W[5], W[6], W[7]);
+                    } else if (inb) {
                         store32(ob + (size_t)r * a.pitch, off, W);
+                    }
                 }
             }(),
             ...);
     }(std::make_integer_sequence<int, 8>{});
-    // every wave's syndrome stores complete before any wave reads them back
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    barrier_lds();
+    barrier_lds();  // the LDS-held chunks are complete
     FP_MARK(6);
 
     // ---------------- phase 2: x = V_E^-1 s (threaded code) ----------------
@@ -275,14 +350,17 @@ __device__ __forceinline__ void run_group(const Args& a, uint4 (*lds)[S * 2 * 64
         return nt > G ? 2 * ((nt - G + NW - 1) / NW) : 0;
     };
     asm volatile(RSGPU_TC_ZERO ::: RSGPU_TC_ACC_CLOBBERS);
-    issue2(0);
     for (int ch = 0; ch < NCH2; ++ch) {
         const int nt = min(S, E - ch * S);
         FP_MARK(10);
-        if (ch + 1 < NCH2) {
+        // chunk ch + 1 >= NLDS comes by LDS-DMA into buffer (ch + 1) & 1,
+        // free since the last barrier; chunk ch >= NLDS was issued one step
+        // ago and must have landed (own pieces; the barrier covers the rest)
+        if (ch + 1 < NCH2 && ch + 1 >= NLDS) {
             issue2(ch + 1);
-            wait_vm(own2(ch + 1));
-        } else {
+            if (ch >= NLDS)
+                wait_vm(own2(ch + 1));
+        } else if (ch >= NLDS) {
             wait_vm(0);
         }
         FP_MARK(7);
@@ -309,6 +387,8 @@ __device__ __forceinline__ void run_group(const Args& a, uint4 (*lds)[S * 2 * 64
         }
 #undef RSGPU_TC_RUN
         FP_MARK(9);
+        if (ch == 0 && G >= NLDS)  // parked syndromes written before chunk NLDS is fetched
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         barrier_lds();  // buffer ch & 1 is refilled by chunk ch + 2
     }
     FP_MARK(10);

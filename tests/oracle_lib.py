@@ -162,10 +162,15 @@ class Reference:
         self._enc_block = L.fn("encode_block", None, C.c_int, C.c_int, C.c_int, vpp, vpp)
         self._dec_block = L.fn("decode_block", C.c_int, C.c_int, C.c_int, C.c_int, u8p,
                                vpp, vpp, vpp)
-        self._bench = L.fn("cpu_bench", C.c_double, C.c_int, C.c_int, C.c_int, C.c_int,
-                           C.c_int, C.c_uint64, C.POINTER(C.c_double),
+        self._bench = L.fn("cpu_bench_kernel", C.c_double, C.c_int, C.c_int, C.c_int, C.c_int,
+                           C.c_int, C.c_uint64, C.c_int, C.POINTER(C.c_double),
                            C.POINTER(C.c_double), C.POINTER(C.c_double),
                            C.POINTER(C.c_int))
+        # the AVX2 restatement of ISA-L's asm data kernel (isal_avx2_port.c)
+        self._enc_avx2 = L.fn("encode_block_avx2", None, C.c_int, C.c_int, C.c_int, vpp, vpp)
+        self._dec_avx2 = L.fn("decode_block_avx2", C.c_int, C.c_int, C.c_int, C.c_int, u8p,
+                              vpp, vpp, vpp)
+        self.have_avx2 = bool(L.fn("have_avx2", C.c_int)())
 
     gen_rs_matrix = Oracle.gen_rs_matrix
     gen_cauchy1_matrix = Oracle.gen_cauchy1_matrix
@@ -178,9 +183,23 @@ class Reference:
     encode_block = Oracle.encode_block
     decode_block = Oracle.decode_block
 
-    def cpu_bench(self, k, e, length, threads, blocks_per_thread, seed=1):
+    def encode_block_avx2(self, data, e: int):
+        k, L = len(data), data[0].shape[0]
+        par = [np.zeros(L, np.uint8) for _ in range(e)]
+        self._enc_avx2(k, e, L, _ptrs(data), _ptrs(par))
+        return par
+
+    def decode_block_avx2(self, data, parity, err_list):
+        k, e, L = len(data), len(parity), data[0].shape[0]
+        err = np.ascontiguousarray(err_list, np.uint8)
+        out = [np.zeros(L, np.uint8) for _ in range(e)]
+        rc = self._dec_avx2(k, e, L, err.ctypes.data, _ptrs(data), _ptrs(parity), _ptrs(out))
+        return rc, out
+
+    def cpu_bench(self, k, e, length, threads, blocks_per_thread, seed=1, kernel=0):
+        """kernel 0: the reference's ec_encode_data_base; 1: the AVX2 port."""
         es, ds, mx, f = C.c_double(), C.c_double(), C.c_double(), C.c_int()
-        wall = self._bench(k, e, length, threads, blocks_per_thread, seed, C.byref(es),
+        wall = self._bench(k, e, length, threads, blocks_per_thread, seed, kernel, C.byref(es),
                            C.byref(ds), C.byref(mx), C.byref(f))
         return {"wall_s": wall, "enc_s": es.value, "dec_s": ds.value,
                 "max_thread_s": mx.value, "failures": f.value}

@@ -1,0 +1,124 @@
+"""The generated GF(2^8) asm (storage-benchmarks_amd/csrc/gen_tc_handlers.py)
+checked on the CPU by interpreting its VALU instructions over bit-sliced
+planes: the 256 threaded-code handlers, the compile-time syndrome MAC blocks,
+the Horner twiddles and the parity pre-scales must multiply exactly as
+gf_mul (isa/ec_base.c:36-48) does.  No GPU needed: a wrong register or plane
+in the generator shows up here before it can corrupt a decode."""
+import os
+import random
+import re
+import sys
+
+import pytest
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                "storage-benchmarks_amd", "csrc"))
+import gen_tc_handlers as g  # noqa: E402
+
+INSN = re.compile(r"(\S+) v(\d+), v(\d+)(?:, v(\d+))?(?:, v(\d+))?")
+
+
+def run(ins, regs):
+    for i in ins:
+        if i.startswith("s_"):
+            continue
+        m = INSN.match(i)
+        assert m, i
+        op, d = m.group(1), int(m.group(2))
+        s = [int(x) for x in m.groups()[2:] if x]
+        if op.startswith("v_mov"):
+            regs[d] = regs[s[0]]
+        elif op.startswith("v_xor"):
+            regs[d] = regs[s[0]] ^ regs[s[1]]
+        elif op.startswith("v_bitop3"):
+            assert i.endswith("bitop3:0x96"), i
+            regs[d] = regs[s[0]] ^ regs[s[1]] ^ regs[s[2]]
+        else:
+            raise AssertionError(i)
+
+
+def planes(by):
+    return [sum(((x >> a) & 1) << i for i, x in enumerate(by)) for a in range(8)]
+
+
+def unplanes(p):
+    return [sum(((p[a] >> i) & 1) << a for a in range(8)) for i in range(32)]
+
+
+def load_tables(regs, by):
+    """The four-Russians tables of one source: single-bit entries = planes,
+    the rest built by the generator's own table code."""
+    p = planes(by)
+    for a, r in enumerate(g.PLANE_REG):
+        regs[r] = p[a]
+    run(g.tables(), regs)
+
+
+@pytest.mark.parametrize("c", range(256))
+def test_handler_multiplies(c):
+    rng = random.Random(c)
+    regs = {i: 0 for i in range(256)}
+    src = [rng.randrange(256) for _ in range(32)]
+    acc = [rng.randrange(256) for _ in range(32)]
+    load_tables(regs, src)
+    for a, v in enumerate(planes(acc)):
+        regs[g.ACC + a] = v
+    body = g.handler(c)
+    assert sum(4 if i.startswith("s_") else 8 for i in body) == g.STRIDE
+    run(body, regs)
+    got = unplanes([regs[g.ACC + a] for a in range(8)])
+    assert got == [x ^ g.gf_mul(c, y) for x, y in zip(acc, src)]
+
+
+def test_lin_inplace_all_constants():
+    rng = random.Random(7)
+    for c in range(1, 256):
+        for slot in (0, 5):
+            regs = {i: 0 for i in range(256)}
+            by = [rng.randrange(256) for _ in range(32)]
+            base = g.ACC + 8 * slot
+            for a, v in enumerate(planes(by)):
+                regs[base + a] = v
+            run(g.lin_inplace(c, slot), regs)
+            assert unplanes([regs[base + a] for a in range(8)]) == [g.gf_mul(c, x) for x in by]
+
+
+@pytest.mark.parametrize("plan", g.SYN_PLANS, ids=lambda p: "K%dE%dC%d" % p)
+def test_syndrome_blocks_horner(plan):
+    """The fused decode's phase 1 (rs_decode_fused.hip) as the kernel runs
+    it: parity rows pre-scaled in the accumulators, then the live sources in
+    Horner order (chunks NCH-1 .. 0) through the SynBlock MACs with one
+    twiddle per chunk boundary -- equals P_r ^ sum_{j live} 2^(r j) d_j."""
+    K, E, C = plan
+    rng = random.Random(K * 1000 + E * 10 + C)
+    data = [[rng.randrange(256) for _ in range(32)] for _ in range(K)]
+    par = [[rng.randrange(256) for _ in range(32)] for _ in range(E)]
+    nch = (K + C - 1) // C
+    erased = set(rng.sample(range(K), E))
+    live = [j for j in range(K) if j not in erased]
+    for grp in range((E + 7) // 8):
+        regs = {i: 0 for i in range(256)}
+        for s in range(8):
+            r = 8 * grp + s
+            if r < E:
+                for a, v in enumerate(planes(par[r])):
+                    regs[g.ACC + 8 * s + a] = v
+        run(g.syn_prescale(K, E, C, grp), regs)
+        for ch in reversed(range(nch)):
+            if ch != nch - 1:
+                run(g.syn_twiddle(E, C, grp), regs)
+            for t in range(C):
+                j = ch * C + t
+                if j < K and j not in erased:
+                    load_tables(regs, data[j])
+                    run(g.syn_block(K, E, grp, t), regs)
+        for s in range(8):
+            r = 8 * grp + s
+            if r >= E:
+                continue
+            exp = list(par[r])
+            for j in live:
+                cj = g.gf_pow2(r * j)
+                exp = [x ^ g.gf_mul(cj, y) for x, y in zip(exp, data[j])]
+            got = unplanes([regs[g.ACC + 8 * s + a] for a in range(8)])
+            assert got == exp, (plan, r)

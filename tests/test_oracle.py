@@ -145,3 +145,28 @@ def test_rs_and_cauchy_matrices_vs_reference():
     for m, k in ((9, 5), (20, 16), (96, 64), (120, 100), (250, 200)):
         assert (orc.gen_rs_matrix(m, k) == ref.gen_rs_matrix(m, k)).all()
         assert (orc.gen_cauchy1_matrix(m, k) == ref.gen_cauchy1_matrix(m, k)).all()
+
+
+@needs_ref
+def test_avx2_port_equals_reference_base():
+    """The CPU baseline's AVX2 data kernel (oracle/isal_avx2_port.c, a
+    restatement of gf_{1..4}vect_dot_prod_avx2 + ec_encode_data_avx2) gives the
+    reference base C's bytes, as ISA-L's own SIMD-vs-base tests require
+    (gf_vect_dot_prod_avx_test.c:162-193): every 4/3/2/1-row pass split and
+    lengths with an overlapped tail."""
+    ref = Reference()
+    if not ref.have_avx2:
+        pytest.skip("host CPU has no AVX2")
+    rng = np.random.default_rng(11)
+    for k, e, L in ((16, 4, 4096), (64, 32, 4096), (100, 20, 1000), (5, 4, 33), (7, 3, 31),
+                    (9, 5, 32), (13, 7, 8191), (3, 1, 100), (30, 2, 65)):
+        data = [rng.integers(0, 256, L, dtype=np.uint8) for _ in range(k)]
+        p_base = ref.encode_block(data, e)
+        p_avx = ref.encode_block_avx2(data, e)
+        assert all((x == y).all() for x, y in zip(p_base, p_avx)), (k, e, L)
+        err = np.sort(rng.choice(k, size=min(e, k), replace=False)).astype(np.uint8)
+        rc1, r1 = ref.decode_block(data, p_base, err)
+        rc2, r2 = ref.decode_block_avx2(data, p_base, err)
+        assert rc1 == rc2 == 0
+        assert all((x == y).all() for x, y in zip(r1, r2))
+        assert all((r2[i] == data[s]).all() for i, s in enumerate(err))

@@ -1,0 +1,11 @@
+# Session-2 GPU call: decode parity + fused profile + bench.
+set -o pipefail
+export TMPDIR=/tmp
+O=gpurun_out/${1:-s2x}
+mkdir -p $O
+T="timeout -k 10"
+$T 300 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 120 --timeout-method thread -k "golden or round_trip or oracle_decode or sign_bit or erasure_counts" > $O/pytest_dec.log 2>&1 && \
+$T 120 ./tools/fused_profile 256 > $O/fused_profile.log 2>&1 && \
+$T 240 python bench.py --steps 5 --warmup 1 --no-cpu-baseline > $O/bench.log 2>&1 && \
+$T 240 python bench.py --steps 5 --warmup 1 --no-cpu-baseline > $O/bench2.log 2>&1
+echo "exit $?"
