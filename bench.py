@@ -150,7 +150,7 @@ def cpu_baseline(k, e, L, threads, kernel=1, blocks_per_thread=None):
     ref = oracle_lib.Reference()
     if kernel == 1 and not ref.have_avx2:
         return {"error": "host CPU has no AVX2"}
-    bpt = blocks_per_thread or (4 if kernel == 1 else 1)
+    bpt = blocks_per_thread or (8 if kernel == 1 else 1)
     r = ref.cpu_bench(k, e, L, threads, bpt, 7, kernel)
     out_bytes = 2.0 * e * L * threads * bpt
     t = r["max_thread_s"]
