@@ -227,23 +227,32 @@ __device__ __forceinline__ void run_group(const Args& a, uint4 (*lds)[S * 2 * 64
     // ---------------- phase 1: syndromes ----------------
     auto first_src = [&](int n) { return (NCH - 1 - n / NP) * C + (n % NP) * S; };
     auto part_len = [&](int n) { return min(S, C - (n % NP) * S); };
-    auto issue1 = [&](int n) {
-        const int j0 = first_src(n), nt = part_len(n);
+    // The live sources of step n are dealt round-robin over the waves by
+    // rank (starting at wave n % NW), so every wave moves and transposes
+    // the same number of rows, +-1, whatever the erasure pattern.
+    auto live_bits = [&](int n) -> uint32_t {  // bit t: slot t of step n is a live source
+        const int j0 = first_src(n);
+        const int nt = min(part_len(n), K - j0);  // slots past K hold nothing
+        const uint64_t er = j0 == 0 ? em0 : j0 < 64 ? (em0 >> j0) | (em1 << (64 - j0)) : em1 >> (j0 - 64);
+        return ~(uint32_t)er & ((1u << nt) - 1);  // nt <= S = 8
+    };
+    auto dealt = [&](int n, uint32_t m) -> uint32_t {  // this wave's slots of step n
+        uint32_t mine = 0;
+        for (int rk = n % NW; m; m &= m - 1, rk = rk + 1 == NW ? 0 : rk + 1)
+            mine |= rk == G ? m & (0u - m) : 0u;
+        return mine;
+    };
+    auto issue1 = [&](int n, uint32_t mine) {
+        const int j0 = first_src(n);
         const uint32_t base = lds0 + (uint32_t)((n & 1) * S * 2 * 64 * 16);
-        for (int t = G; t < nt; t += NW)
-            if (live(j0 + t)) {
-                const uint8_t* row = sb + (size_t)(j0 + t) * a.pitch + loff;
-                glds16(row, base + (uint32_t)((t * 2 + 0) * 64 * 16));
-                glds16(row + 16, base + (uint32_t)((t * 2 + 1) * 64 * 16));
-            }
+        for (; mine; mine &= mine - 1) {
+            const int t = __builtin_ctz(mine);
+            const uint8_t* row = sb + (size_t)(j0 + t) * a.pitch + loff;
+            glds16(row, base + (uint32_t)((t * 2 + 0) * 64 * 16));
+            glds16(row + 16, base + (uint32_t)((t * 2 + 1) * 64 * 16));
+        }
     };
-    auto issued1 = [&](int n) {
-        const int j0 = first_src(n), nt = part_len(n);
-        int c = 0;
-        for (int t = G; t < nt; t += NW)
-            c += live(j0 + t) ? 2 : 0;
-        return c;
-    };
+    auto issued1 = [&](uint32_t mine) { return 2 * __builtin_popcount(mine); };
 
     FP_DECL
     asm volatile(RSGPU_TC_ZERO ::: RSGPU_TC_ACC_CLOBBERS);
@@ -254,8 +263,9 @@ __device__ __forceinline__ void run_group(const Args& a, uint4 (*lds)[S * 2 * 64
                          : void()),
          ...);
     }(std::make_integer_sequence<int, 8>{});
-    issue1(0);
-    wait_vm(issued1(0));  // the (older) parity loads have landed
+    uint32_t mine_next = dealt(0, live_bits(0));
+    issue1(0, mine_next);
+    wait_vm(issued1(mine_next));  // the (older) parity loads have landed
     // bytes -> planes, scaled by 2^(-C r (NCH-1)): the NCH-1 Horner twiddles
     // of the chunk loop bring them back to P_r
     [&]<int... Ss>(std::integer_sequence<int, Ss...>) {
@@ -273,25 +283,27 @@ __device__ __forceinline__ void run_group(const Args& a, uint4 (*lds)[S * 2 * 64
     syn_prescale<K, E, C, NW>(G);
     for (int n = 0; n < NSTEP; ++n) {
         uint4* buf = lds[n & 1];
-        const int j0 = first_src(n), nt = part_len(n);
+        const int j0 = first_src(n);
+        const uint32_t mine = mine_next;
         FP_MARK(5);
         if (n + 1 < NSTEP) {
-            issue1(n + 1);
+            mine_next = dealt(n + 1, live_bits(n + 1));
+            issue1(n + 1, mine_next);
             FP_MARK(0);
-            wait_vm(issued1(n + 1));
+            wait_vm(issued1(mine_next));
         } else {
             wait_vm(0);
         }
         FP_MARK(1);
-        for (int t = G; t < nt; t += NW)
-            if (live(j0 + t)) {
-                uint4 u = buf[(t * 2 + 0) * 64 + lane];
-                uint4 v = buf[(t * 2 + 1) * 64 + lane];
-                uint32_t W[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
-                tr8(W, m4, m2, m1);
-                buf[(t * 2 + 0) * 64 + lane] = make_uint4(W[0], W[1], W[2], W[3]);
-                buf[(t * 2 + 1) * 64 + lane] = make_uint4(W[4], W[5], W[6], W[7]);
-            }
+        for (uint32_t mm = mine; mm; mm &= mm - 1) {
+            const int t = __builtin_ctz(mm);
+            uint4 u = buf[(t * 2 + 0) * 64 + lane];
+            uint4 v = buf[(t * 2 + 1) * 64 + lane];
+            uint32_t W[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
+            tr8(W, m4, m2, m1);
+            buf[(t * 2 + 0) * 64 + lane] = make_uint4(W[0], W[1], W[2], W[3]);
+            buf[(t * 2 + 1) * 64 + lane] = make_uint4(W[4], W[5], W[6], W[7]);
+        }
         FP_MARK(2);
         barrier_lds();
         FP_MARK(3);
