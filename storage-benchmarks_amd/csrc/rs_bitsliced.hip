@@ -269,11 +269,9 @@ __device__ __forceinline__ void run_group(const Args& a, uint4 (*lds)[S * 2 * 64
         const int j0 = first_src(n), nt = part_len(n);
         const uint32_t base = lds0 + (uint32_t)((n & 1) * S * 2 * 64 * 16);
         for (int t = G; t < nt; t += NW)
-            if (live(j0 + t)) {
-                const uint8_t* row = sb + (size_t)(j0 + t) * a.pitch + loff;
-                bs::glds16(row, base + (uint32_t)((t * 2 + 0) * 64 * 16));
-                bs::glds16(row + 16, base + (uint32_t)((t * 2 + 1) * 64 * 16));
-            }
+            if (live(j0 + t))
+                bs::glds32(sb + (size_t)(j0 + t) * a.pitch, (uint32_t)loff,
+                           base + (uint32_t)(t * 2 * 64 * 16));
     };
     auto issued = [&](int n) {
         const int j0 = first_src(n), nt = part_len(n);

@@ -46,7 +46,7 @@ struct XorSlot;
 #include "syn_blocks.inc"
 
 using bs::barrier_lds;
-using bs::glds16;
+using bs::glds32;
 using bs::store32;
 using bs::tr8;
 using bs::vconst;
@@ -247,9 +247,7 @@ __device__ __forceinline__ void run_group(const Args& a, uint4 (*lds)[S * 2 * 64
         const uint32_t base = lds0 + (uint32_t)((n & 1) * S * 2 * 64 * 16);
         for (; mine; mine &= mine - 1) {
             const int t = __builtin_ctz(mine);
-            const uint8_t* row = sb + (size_t)(j0 + t) * a.pitch + loff;
-            glds16(row, base + (uint32_t)((t * 2 + 0) * 64 * 16));
-            glds16(row + 16, base + (uint32_t)((t * 2 + 1) * 64 * 16));
+            glds32(sb + (size_t)(j0 + t) * a.pitch, (uint32_t)loff, base + (uint32_t)(t * 2 * 64 * 16));
         }
     };
     auto issued1 = [&](uint32_t mine) { return 2 * __builtin_popcount(mine); };
@@ -352,9 +350,7 @@ __device__ __forceinline__ void run_group(const Args& a, uint4 (*lds)[S * 2 * 64
         const int c0 = ch * S, nt = min(S, E - c0);
         const uint32_t base = lds0 + (uint32_t)((ch & 1) * S * 2 * 64 * 16);
         for (int t = G; t < nt; t += NW) {
-            const uint8_t* row = ob + (size_t)(c0 + t) * a.pitch + loff;
-            glds16(row, base + (uint32_t)((t * 2 + 0) * 64 * 16));
-            glds16(row + 16, base + (uint32_t)((t * 2 + 1) * 64 * 16));
+            glds32(ob + (size_t)(c0 + t) * a.pitch, (uint32_t)loff, base + (uint32_t)(t * 2 * 64 * 16));
         }
     };
     auto own2 = [&](int ch) {
