@@ -339,3 +339,41 @@ def test_syndrome_decode_sign_bit_masks(ctx, k, e, pattern):
     torch.cuda.synchronize()
     assert dec.is_complete()
     assert dec.verify_data(enc)
+
+
+def test_isa_arithmetic_peer():
+    """bin/rs_arithmetic (peer of benchmark/isa_arithmetic) runs every
+    benchmark of the reference's sweep and checks that the 1/2/4/all-row pass
+    splits give identical outputs (the runner exits non-zero otherwise)."""
+    import subprocess
+    exe = os.path.join(os.path.dirname(HERE), "storage-benchmarks_amd", "bin", "rs_arithmetic")
+    out = subprocess.run([exe, "--size", "65536", "1000", "--vectors", "8", "13", "32"],
+                         capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("ISA/")]
+    assert len(lines) == 2 * 3 * 4
+    for name in ("dot_product1", "dot_product2", "dot_product4", "dot_product_encode"):
+        assert sum(name + " " in ln for ln in lines) == 6
+
+
+@pytest.mark.parametrize("length", [1000, 1024, 992, 100, 65536])
+@pytest.mark.parametrize("per", [1, 2, 4, 8])
+def test_ec_encode_data_row_passes(ctx, orc, length, per):
+    """ec_encode_data called in passes of `per` output rows, as
+    ec_encode_data_avx2 splits them (ec_highlevel_func.c:106-135) and
+    isa_arithmetic's dot_product1/2/4 drive them, back to back on one
+    stream: every pass equals the oracle."""
+    rng = np.random.default_rng(length * 10 + per)
+    k = rows = 8
+    a = orc.gen_rs_matrix(2 * k, k)
+    g = orc.init_tables(k, rows, a[k:])
+    data = [rng.integers(0, 256, length, dtype=np.uint8) for _ in range(k)]
+    d_data = [dev(d) for d in data]
+    d_out = [torch.zeros(length, dtype=torch.uint8, device="cuda") for _ in range(rows)]
+    for r in range(0, rows, per):
+        ctx.ec_encode_data(length, k, per, g[r * k * 32:], d_data, d_out[r:r + per])
+    torch.cuda.synchronize()
+    ref = [np.zeros(length, np.uint8) for _ in range(rows)]
+    orc.encode_data(length, k, rows, g, data, ref)
+    bad = [r for r in range(rows) if not (d_out[r].cpu().numpy() == ref[r]).all()]
+    assert not bad, f"rows {bad} differ"
