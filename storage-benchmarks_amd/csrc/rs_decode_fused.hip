@@ -252,10 +252,12 @@ __device__ __forceinline__ void run_group(const Args& a, uint4 (*lds)[S * 2 * 64
     };
     auto issued1 = [&](uint32_t mine) { return 2 * __builtin_popcount(mine); };
 
+    // Parity rows straight into this wave's accumulators; their latency
+    // overlaps the first two LDS-DMA parts.  (Streaming one parity row per
+    // step instead, scaled for the twiddles still to come, removed this
+    // prologue but measured 1-2 % slower overall.)
     FP_DECL
     asm volatile(RSGPU_TC_ZERO ::: RSGPU_TC_ACC_CLOBBERS);
-    // parity rows straight into this wave's accumulators; their latency
-    // overlaps the first LDS-DMA part
     [&]<int... Ss>(std::integer_sequence<int, Ss...>) {
         ((G * 8 + Ss < E ? load_slot<Ss>(a.par + ((size_t)b * E + G * 8 + Ss) * a.pitch + loff)
                          : void()),
@@ -263,7 +265,11 @@ __device__ __forceinline__ void run_group(const Args& a, uint4 (*lds)[S * 2 * 64
     }(std::make_integer_sequence<int, 8>{});
     uint32_t mine_next = dealt(0, live_bits(0));
     issue1(0, mine_next);
-    wait_vm(issued1(mine_next));  // the (older) parity loads have landed
+    // buffer 1 is free from the start: part 1 flies during the parity work
+    const uint32_t mine1 = NSTEP > 1 ? dealt(1, live_bits(1)) : 0u;
+    if (NSTEP > 1)
+        issue1(1, mine1);
+    wait_vm(issued1(mine_next) + issued1(mine1));  // the (older) parity loads have landed
     // bytes -> planes, scaled by 2^(-C r (NCH-1)): the NCH-1 Horner twiddles
     // of the chunk loop bring them back to P_r
     [&]<int... Ss>(std::integer_sequence<int, Ss...>) {
@@ -279,12 +285,17 @@ __device__ __forceinline__ void run_group(const Args& a, uint4 (*lds)[S * 2 * 64
             ...);
     }(std::make_integer_sequence<int, 8>{});
     syn_prescale<K, E, C, NW>(G);
+    FP_MARK(12);
     for (int n = 0; n < NSTEP; ++n) {
         uint4* buf = lds[n & 1];
         const int j0 = first_src(n);
         const uint32_t mine = mine_next;
         FP_MARK(5);
-        if (n + 1 < NSTEP) {
+        if (n == 0 && NSTEP > 1) {  // part 1 already issued in the prologue
+            mine_next = mine1;
+            FP_MARK(0);
+            wait_vm(issued1(mine_next));
+        } else if (n + 1 < NSTEP) {
             mine_next = dealt(n + 1, live_bits(n + 1));
             issue1(n + 1, mine_next);
             FP_MARK(0);

@@ -81,7 +81,7 @@ int main(int argc, char** argv)
     const char* names[16] = {"p1 issue DMA", "p1 wait vmcnt", "p1 transpose in", "p1 barrier 1",
                              "p1 syndrome MAC", "p1 barrier 2+loop", "parity+syn store",
                              "p2 issue+wait", "p2 barrier 1", "p2 chunk asm", "p2 barrier 2+loop",
-                             "output store", "", "", "", "wave lifetime"};
+                             "output store", "prologue (parity)", "", "", "wave lifetime"};
     printf("k_rs_decode_fused<64,32>: B=%d L=%lld  %.3f ms  (%.1f GB/s alg)\n", B, L, ms,
            (double)(k + e) * L * B / (ms * 1e-3) / 1e9);
     for (int i = 0; i < 16; ++i)

@@ -42,6 +42,16 @@ __global__ __launch_bounds__(256) void kern(uint32_t* out, unsigned long long* c
         if constexpr (OP == 13) BODY(asm volatile("v_mov_b32 %0, %1" : "=v"(r[i]) : "v"(r[(i + 1) & 15])))
         if constexpr (OP == 14) BODY(asm volatile("v_pk_add_u16 %0, %0, %1" : "+v"(r[i]) : "v"(t[i])))
         if constexpr (OP == 15) BODY(asm volatile("v_cndmask_b32 %0, %0, %1, vcc" : "+v"(r[i]) : "v"(t[i])))
+        if constexpr (OP == 16) {
+            // 64-bit shifts on register pairs (8 pairs = the 16 chains)
+            _Pragma("unroll") for (int i = 0; i < 16; i += 2) {
+                unsigned long long x = ((unsigned long long)r[i + 1] << 32) | r[i];
+                asm volatile("v_lshlrev_b64 %0, 4, %0" : "+v"(x));
+                asm volatile("v_lshrrev_b64 %0, 2, %0" : "+v"(x));
+                r[i] = (uint32_t)x;
+                r[i + 1] = (uint32_t)(x >> 32);
+            }
+        }
     }
     unsigned long long t1 = __builtin_amdgcn_s_memtime();
     unsigned long long r1 = __builtin_amdgcn_s_memrealtime();
@@ -104,6 +114,7 @@ int main()
         run<9>("v_alignbit", w, d, c);
         run<13>("v_mov", w, d, c);
         run<15>("v_cndmask", w, d, c);
+        run<16>("v_lshl/rrev_b64", w, d, c);
     }
     return 0;
 }
