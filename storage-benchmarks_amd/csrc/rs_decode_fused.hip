@@ -26,6 +26,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <cstdlib>
+#include <cstring>
 #include <utility>
 
 #include "bitslice.h"
@@ -91,6 +93,7 @@ struct Args {
     long long pitch, len;
     const uint64_t* emask;             // [B][2] erased originals
     const unsigned long long* addr;    // [B][E][8 NW] handler addresses of V_E^-1
+    const unsigned long long* syn_addr;  // [B][K-E][8 NW] handlers of 2^(r j), survivors j
     const int* status;                 // [B]
 };
 
@@ -203,11 +206,38 @@ __device__ __forceinline__ void syn_part(int G, const uint4* buf, int lane, int 
     }(std::make_integer_sequence<int, S>{});
 }
 
+// One LDS part of nt sources through the threaded-code chunk asm
+// (gen_tc_handlers.py): la = part base + 16 lane, pa = this wave's handler
+// addresses of the part's first source (NW * 8 per source).
+template <int NW>
+__device__ __forceinline__ void tc_chunk(uint32_t la, const unsigned long long* pa, int nt)
+{
+#define RSGPU_TC_RUN(N)                                                                          \
+    asm volatile(RSGPU_TC_CHUNK##N                                                               \
+                 :                                                                               \
+                 : [la] "v"(la), [pa] "s"(pa), [o1] "i"(1 * NW * 64), [o2] "i"(2 * NW * 64),      \
+                   [o3] "i"(3 * NW * 64), [o4] "i"(4 * NW * 64), [o5] "i"(5 * NW * 64),           \
+                   [o6] "i"(6 * NW * 64), [o7] "i"(7 * NW * 64)                                  \
+                 : RSGPU_TC_CLOBBERS, RSGPU_TC_ACC_CLOBBERS, "memory")
+    switch (nt) {
+    case 1: RSGPU_TC_RUN(1); break;
+    case 2: RSGPU_TC_RUN(2); break;
+    case 3: RSGPU_TC_RUN(3); break;
+    case 4: RSGPU_TC_RUN(4); break;
+    case 5: RSGPU_TC_RUN(5); break;
+    case 6: RSGPU_TC_RUN(6); break;
+    case 7: RSGPU_TC_RUN(7); break;
+    default: RSGPU_TC_RUN(8); break;
+    }
+#undef RSGPU_TC_RUN
+}
+
 // The scaffolding is shared by every wave group (G runtime, wave-uniform):
 // only the generated MAC / twiddle blocks differ per group, which keeps the
 // executed code of all groups plus the 256 handlers inside the I-cache.
-template <int K, int E, int C, int NW>
-__device__ __forceinline__ void run_group(const Args& a, uint4 (*lds)[S * 2 * 64], int G)
+template <int K, int E, int C, int NW, bool TC1>
+__device__ __forceinline__ void run_group(const Args& a, uint4 (*lds)[S * 2 * 64], uint8_t* items,
+                                          int G)
 {
     constexpr int NCH = (K + C - 1) / C;
     constexpr int NP = (C + S - 1) / S;
@@ -225,6 +255,110 @@ __device__ __forceinline__ void run_group(const Args& a, uint4 (*lds)[S * 2 * 64
     const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint4*)&lds[0][0];
 
     // ---------------- phase 1: syndromes ----------------
+    FP_DECL
+    if constexpr (TC1) {
+        // Threaded code (the phase-2 machinery): the K-E survivors in
+        // ascending order, S per LDS part, each wave moving and transposing
+        // slots t = G, G+NW, ...; coefficient 2^(r j) of survivor j for
+        // syndrome row r comes as a handler address from the prepare
+        // kernel's table.  No Horner chunks, so no twiddles and the parity
+        // rows enter the accumulators unscaled.
+        constexpr int NL = K - E;
+        constexpr int NSTEP = (NL + S - 1) / S;
+        static_assert(K <= 128, "survivor list: one byte per survivor, two lanes' words");
+        uint32_t vi0 = 0, vi1 = 0;  // lane q: survivor q (q < 64) / 64 + q
+        {
+            auto range = [](int lo, int hi) -> uint64_t {  // bits [lo, hi) of one word
+                lo = max(lo, 0);
+                hi = min(hi, 64);
+                if (hi <= lo)
+                    return 0;
+                const uint64_t below_hi = hi >= 64 ? ~0ull : ((1ull << hi) - 1);
+                return below_hi & ~((1ull << lo) - 1);
+            };
+            const uint64_t lv0 = ~em0 & range(0, K), lv1 = ~em1 & range(0, K - 64);
+            for (int j = lane; j < K; j += 64)
+                if (live(j))
+                    items[__popcll(lv0 & range(0, j)) + __popcll(lv1 & range(-64, j - 64))] = (uint8_t)j;
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // own lanes' writes, in order
+            vi0 = lane < NL ? items[lane] : 0;
+            if constexpr (NL > 64)
+                vi1 = 64 + lane < NL ? items[64 + lane] : 0;
+        }
+        auto survivor = [&](int q) -> int {
+            if constexpr (NL > 64)
+                return __builtin_amdgcn_readlane((int)(q < 64 ? vi0 : vi1), q & 63);
+            return __builtin_amdgcn_readlane((int)vi0, q);
+        };
+        auto part_n = [&](int n) { return min(S, NL - n * S); };
+        auto issue1 = [&](int n) {
+            const uint32_t base = lds0 + (uint32_t)((n & 1) * S * 2 * 64 * 16);
+            for (int t = G; t < part_n(n); t += NW)
+                glds32(sb + (size_t)survivor(n * S + t) * a.pitch, (uint32_t)loff,
+                       base + (uint32_t)(t * 2 * 64 * 16));
+        };
+        auto own1 = [&](int n) {
+            const int nt = part_n(n);
+            return nt > G ? 2 * ((nt - G + NW - 1) / NW) : 0;
+        };
+        asm volatile(RSGPU_TC_ZERO ::: RSGPU_TC_ACC_CLOBBERS);
+        // parity rows straight into this wave's accumulators (unscaled)
+        [&]<int... Ss>(std::integer_sequence<int, Ss...>) {
+            ((G * 8 + Ss < E ? load_slot<Ss>(a.par + ((size_t)b * E + G * 8 + Ss) * a.pitch + loff)
+                             : void()),
+             ...);
+        }(std::make_integer_sequence<int, 8>{});
+        issue1(0);
+        if (NSTEP > 1)
+            issue1(1);
+        wait_vm(own1(0) + (NSTEP > 1 ? own1(1) : 0));  // the (older) parity loads have landed
+        [&]<int... Ss>(std::integer_sequence<int, Ss...>) {
+            (
+                [&] {
+                    if (G * 8 + Ss < E) {
+                        uint32_t W[8];
+                        read_slot<Ss>(W);
+                        tr8(W, m4, m2, m1);
+                        write_slot<Ss>(W);
+                    }
+                }(),
+                ...);
+        }(std::make_integer_sequence<int, 8>{});
+        FP_MARK(12);
+        const unsigned long long* sp = a.syn_addr + (size_t)b * NL * (NW * 8) + G * 8;
+        for (int n = 0; n < NSTEP; ++n) {
+            const int nt = part_n(n);
+            FP_MARK(5);
+            if (n == 0) {
+                FP_MARK(0);
+                wait_vm(NSTEP > 1 ? own1(1) : 0);
+            } else if (n + 1 < NSTEP) {
+                issue1(n + 1);
+                FP_MARK(0);
+                wait_vm(own1(n + 1));
+            } else {
+                wait_vm(0);
+            }
+            FP_MARK(1);
+            uint4* buf = lds[n & 1];
+            for (int t = G; t < nt; t += NW) {
+                uint4 u = buf[(t * 2 + 0) * 64 + lane];
+                uint4 v = buf[(t * 2 + 1) * 64 + lane];
+                uint32_t W[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
+                tr8(W, m4, m2, m1);
+                buf[(t * 2 + 0) * 64 + lane] = make_uint4(W[0], W[1], W[2], W[3]);
+                buf[(t * 2 + 1) * 64 + lane] = make_uint4(W[4], W[5], W[6], W[7]);
+            }
+            FP_MARK(2);
+            barrier_lds();
+            FP_MARK(3);
+            tc_chunk<NW>(lds0 + (uint32_t)((n & 1) * S * 2 * 64 * 16) + lane * 16,
+                         sp + (size_t)(n * S) * (NW * 8), nt);
+            FP_MARK(4);
+            barrier_lds();  // buffer n & 1 is refilled by part n + 2
+        }
+        FP_MARK(5);
+    } else {
     auto first_src = [&](int n) { return (NCH - 1 - n / NP) * C + (n % NP) * S; };
     auto part_len = [&](int n) { return min(S, C - (n % NP) * S); };
     // The live sources of step n are dealt round-robin over the waves by
@@ -256,7 +390,6 @@ __device__ __forceinline__ void run_group(const Args& a, uint4 (*lds)[S * 2 * 64
     // overlaps the first two LDS-DMA parts.  (Streaming one parity row per
     // step instead, scaled for the twiddles still to come, removed this
     // prologue but measured 1-2 % slower overall.)
-    FP_DECL
     asm volatile(RSGPU_TC_ZERO ::: RSGPU_TC_ACC_CLOBBERS);
     [&]<int... Ss>(std::integer_sequence<int, Ss...>) {
         ((G * 8 + Ss < E ? load_slot<Ss>(a.par + ((size_t)b * E + G * 8 + Ss) * a.pitch + loff)
@@ -327,6 +460,8 @@ __device__ __forceinline__ void run_group(const Args& a, uint4 (*lds)[S * 2 * 64
     }
     FP_MARK(5);
 
+    }
+
     // The syndromes (parity included), in plane form, are phase 2's sources:
     // wave G's rows are its chunk G.  Waves 0 and 1 write theirs straight
     // into the two LDS part buffers (both free after the last barrier);
@@ -387,24 +522,7 @@ __device__ __forceinline__ void run_group(const Args& a, uint4 (*lds)[S * 2 * 64
         FP_MARK(8);
         const uint32_t la = lds0 + (uint32_t)((ch & 1) * S * 2 * 64 * 16) + lane * 16;
         const unsigned long long* pa = ap + (size_t)(ch * S) * (NW * 8);
-#define RSGPU_TC_RUN(N)                                                                          \
-    asm volatile(RSGPU_TC_CHUNK##N                                                               \
-                 :                                                                               \
-                 : [la] "v"(la), [pa] "s"(pa), [o1] "i"(1 * NW * 64), [o2] "i"(2 * NW * 64),      \
-                   [o3] "i"(3 * NW * 64), [o4] "i"(4 * NW * 64), [o5] "i"(5 * NW * 64),           \
-                   [o6] "i"(6 * NW * 64), [o7] "i"(7 * NW * 64)                                  \
-                 : RSGPU_TC_CLOBBERS, RSGPU_TC_ACC_CLOBBERS, "memory")
-        switch (nt) {
-        case 1: RSGPU_TC_RUN(1); break;
-        case 2: RSGPU_TC_RUN(2); break;
-        case 3: RSGPU_TC_RUN(3); break;
-        case 4: RSGPU_TC_RUN(4); break;
-        case 5: RSGPU_TC_RUN(5); break;
-        case 6: RSGPU_TC_RUN(6); break;
-        case 7: RSGPU_TC_RUN(7); break;
-        default: RSGPU_TC_RUN(8); break;
-        }
-#undef RSGPU_TC_RUN
+tc_chunk<NW>(la, pa, nt);
         FP_MARK(9);
         if (ch == 0 && G >= NLDS)  // parked syndromes written before chunk NLDS is fetched
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -435,23 +553,40 @@ __device__ __forceinline__ void run_group(const Args& a, uint4 (*lds)[S * 2 * 64
     FP_END;
 }
 
-template <int K, int E, int C>
+template <int K, int E, int C, bool TC1>
 __global__ __launch_bounds__(64 * ((E + 7) / 8)) __attribute__((amdgpu_num_vgpr(64))) void
 k_rs_decode_fused(Args a)
 {
     constexpr int NW = (E + 7) / 8;
     __shared__ uint4 lds[2][S * 2 * 64];
+    __shared__ uint8_t items[NW][128];  // per-wave survivor list (TC1)
     if (a.status[blockIdx.y] != 0)
         return;  // singular or malformed: the whole block is skipped
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    run_group<K, E, C, NW>(a, lds, wave);
+    run_group<K, E, C, NW, TC1>(a, lds, items[wave], wave);
+}
+
+// Syndrome phase: threaded code (default) or the compile-time Horner blocks
+// (RSGPU_FUSED_SYN=horner, kept for comparison).
+bool fused_syn_tc()
+{
+    static const bool tc = [] {
+        const char* v = std::getenv("RSGPU_FUSED_SYN");
+        return !(v && std::strcmp(v, "horner") == 0);
+    }();
+    return tc;
 }
 
 template <int K, int E, int C>
 hipError_t launch(const Args& a, long long blocks, hipStream_t st)
 {
     dim3 grid((unsigned)((a.len + 2047) / 2048), (unsigned)blocks);
-    hipLaunchKernelGGL((k_rs_decode_fused<K, E, C>), grid, dim3(64 * ((E + 7) / 8)), 0, st, a);
+    if (fused_syn_tc() && a.syn_addr)
+        hipLaunchKernelGGL((k_rs_decode_fused<K, E, C, true>), grid, dim3(64 * ((E + 7) / 8)), 0,
+                           st, a);
+    else
+        hipLaunchKernelGGL((k_rs_decode_fused<K, E, C, false>), grid, dim3(64 * ((E + 7) / 8)), 0,
+                           st, a);
     return hipGetLastError();
 }
 
@@ -467,9 +602,10 @@ bool rs_decode_fused_available(int k, int e)
 hipError_t launch_rs_decode_fused(int k, int e, const uint8_t* src, const uint8_t* par,
                                   uint8_t* out, long long pitch, long long len, long long blocks,
                                   const uint64_t* emask, const unsigned long long* addr,
-                                  const int* status, hipStream_t st)
+                                  const unsigned long long* syn_addr, const int* status,
+                                  hipStream_t st)
 {
-    fused::Args a{src, par, out, pitch, len, emask, addr, status};
+    fused::Args a{src, par, out, pitch, len, emask, addr, syn_addr, status};
     if (k == 16 && e == 4) return fused::launch<16, 4, 8>(a, blocks, st);
     if (k == 16 && e == 8) return fused::launch<16, 8, 8>(a, blocks, st);
     if (k == 64 && e == 32) return fused::launch<64, 32, 8>(a, blocks, st);

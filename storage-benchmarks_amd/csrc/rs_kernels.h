@@ -57,14 +57,17 @@ hipError_t launch_rs_bitsliced(int k, int e, const uint8_t* src, const uint8_t* 
 // Syndrome-decode prepare: per block, emask, V_E^-1 and its consumers' tables:
 // k_dot_generic tables (tabs4/ctab, when non-null) and/or k_rs_tc handler
 // addresses (tc_addr [B][e][tc_rows], when non-null; tc_table = the 256
-// handler addresses).
+// handler addresses).  syn_addr (non-null with tc_table): [B][k-e][tc_rows]
+// handler addresses of the syndrome rows 2^(r j) per surviving original j
+// (ascending), for the fused decode's threaded-code syndrome phase.
 hipError_t launch_decode_prepare_syn(int k, int e, int rows_pad, long long blocks,
                                      const uint8_t* err, uint8_t* out, long long out_pitch,
                                      const uint8_t** srcs, uint8_t** dsts, uint4* tabs4,
                                      uint32_t* ctab, long long tab_block_stride,
                                      const unsigned long long* tc_table,
                                      unsigned long long* tc_addr, int tc_rows,
-                                     unsigned long long* emask, int* status, hipStream_t st);
+                                     unsigned long long* emask, int* status,
+                                     unsigned long long* syn_addr, hipStream_t st);
 
 // Threaded-code bit-sliced dot product with runtime coefficients (rs_tc.hip):
 // dsts[b][i] = sum_p c_b[i][p] * srcs[b][p] for rows <= 32, where the
@@ -90,7 +93,8 @@ bool rs_decode_fused_available(int k, int e);
 hipError_t launch_rs_decode_fused(int k, int e, const uint8_t* src, const uint8_t* par,
                                   uint8_t* out, long long pitch, long long len, long long blocks,
                                   const uint64_t* emask, const unsigned long long* addr,
-                                  const int* status, hipStream_t st);
+                                  const unsigned long long* syn_addr, const int* status,
+                                  hipStream_t st);
 int tc_handler_stride();
 hipError_t tc_query_handlers(unsigned long long* d_out, hipStream_t st);
 hipError_t launch_rs_tc(const TcArgs& a, long long blocks, hipStream_t st);

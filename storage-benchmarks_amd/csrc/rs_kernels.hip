@@ -820,7 +820,8 @@ __global__ __launch_bounds__(256) void k_decode_prepare_syn(int k, int e, int ro
                                                             long long tab_block_stride,
                                                             const unsigned long long* tc_table,
                                                             unsigned long long* tc_addr, int tc_rows,
-                                                            unsigned long long* emask, int* status)
+                                                            unsigned long long* emask, int* status,
+                                                            unsigned long long* syn_addr)
 {
     extern __shared__ __align__(16) uint8_t lds[];
     uint8_t* gexp = lds;          // 512
@@ -943,6 +944,29 @@ __global__ __launch_bounds__(256) void k_decode_prepare_syn(int k, int e, int ro
     }
     if (st != 0)
         return;
+    if (syn_addr && tc_table) {
+        // syndrome phase of the fused decode (threaded code): the q-th
+        // surviving original j_q (ascending) carries coefficient 2^(r j_q)
+        // for syndrome row r = slot (gf_gen_rs_matrix row k + r,
+        // isa/ec_base.c:71-78); [q][slot], padding slots -> handler 0
+        uint8_t* lv = Dm + e * e;  // live list, k - e bytes
+        for (int j = tid; j < k; j += nt) {
+            int below = 0;  // erased originals < j (the list is validated ascending)
+            bool er = false;
+            for (int i = 0; i < e; ++i) {
+                below += eb[i] < j;
+                er |= eb[i] == j;
+            }
+            if (!er)
+                lv[j - below] = (uint8_t)j;
+        }
+        __syncthreads();
+        unsigned long long* sa = syn_addr + (size_t)b * (k - e) * tc_rows;
+        for (int idx = tid; idx < (k - e) * tc_rows; idx += nt) {
+            const int q = idx / tc_rows, r = idx - q * tc_rows;
+            sa[idx] = tc_table[r < e ? gexp[(r * (int)lv[q]) % 255] : 0];
+        }
+    }
     if (tc_addr) {
         // handler addresses [p][slot]: coefficient (V_E^-1)[slot][p], padding
         // slots -> handler 0 (no-op)
@@ -981,7 +1005,7 @@ __global__ __launch_bounds__(256) void k_decode_prepare_syn(int k, int e, int ro
     }
 }
 
-size_t decode_prepare_syn_lds_bytes(int e) { return 832 + 2 * (size_t)e * e; }
+size_t decode_prepare_syn_lds_bytes(int e) { return 832 + 2 * (size_t)e * e + 256; }
 
 hipError_t launch_decode_prepare_syn(int k, int e, int rows_pad, long long blocks,
                                      const uint8_t* err, uint8_t* out, long long out_pitch,
@@ -989,7 +1013,8 @@ hipError_t launch_decode_prepare_syn(int k, int e, int rows_pad, long long block
                                      uint32_t* ctab, long long tab_block_stride,
                                      const unsigned long long* tc_table,
                                      unsigned long long* tc_addr, int tc_rows,
-                                     unsigned long long* emask, int* status, hipStream_t st)
+                                     unsigned long long* emask, int* status,
+                                     unsigned long long* syn_addr, hipStream_t st)
 {
     static bool attr_set = false;
     if (!attr_set) {
@@ -1000,7 +1025,7 @@ hipError_t launch_decode_prepare_syn(int k, int e, int rows_pad, long long block
     hipLaunchKernelGGL(k_decode_prepare_syn, dim3((unsigned)blocks), dim3(256),
                        decode_prepare_syn_lds_bytes(e), st, k, e, rows_pad, err, out, out_pitch,
                        srcs, dsts, tabs4, ctab, tab_block_stride, tc_table, tc_addr, tc_rows,
-                       emask, status);
+                       emask, status, syn_addr);
     return hipGetLastError();
 }
 

@@ -813,7 +813,8 @@ static bool use_syn_path(int k, int e, size_t len, size_t pitch, const void* src
 }
 
 static void decode_ws_layout(int k, int e, size_t blocks, size_t* off_surv, size_t* off_out,
-                             size_t* off_t4, size_t* off_tc, size_t* off_tca, size_t* total)
+                             size_t* off_t4, size_t* off_tc, size_t* off_tca, size_t* off_sa,
+                             size_t* total)
 {
     const int rows_pad = rows_pad_for(e);
     size_t o = 16 * blocks;  // emask [blocks][2] u64 at offset 0
@@ -828,6 +829,10 @@ static void decode_ws_layout(int k, int e, size_t blocks, size_t* off_surv, size
     o = align_up(o + sizeof(uint32_t) * (size_t)k * rows_pad * blocks, 256);
     *off_tca = o;  // k_rs_tc handler addresses [blocks][e][tc_rows]
     o = align_up(o + sizeof(unsigned long long) * (size_t)e * tc_rows_per_pass(e) * blocks, 256);
+    *off_sa = o;  // fused decode: syndrome-phase handler addresses [blocks][k-e][tc_rows]
+    o = align_up(o + sizeof(unsigned long long) * (size_t)(k > e ? k - e : 0) * tc_rows_per_pass(e) *
+                         blocks,
+                 256);
     *total = o;
 }
 
@@ -835,8 +840,8 @@ size_t rsgpu_decode_workspace_bytes(int k, int e, size_t blocks)
 {
     if (k <= 0 || e <= 0)
         return 256;
-    size_t a, b, c, d, x, t;
-    decode_ws_layout(k, e, blocks, &a, &b, &c, &d, &x, &t);
+    size_t a, b, c, d, x, y, t;
+    decode_ws_layout(k, e, blocks, &a, &b, &c, &d, &x, &y, &t);
     return t;
 }
 
@@ -852,8 +857,8 @@ int rsgpu_decode_prepare(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch,
         return RSGPU_OK;
     if (e > k || !d_err || !d_workspace || !d_status)
         return fail(ctx, RSGPU_ERR_ARG, "rsgpu_decode_prepare: bad arguments");
-    size_t o_surv, o_out, o_t4, o_tc, o_tca, total;
-    decode_ws_layout(k, e, blocks, &o_surv, &o_out, &o_t4, &o_tc, &o_tca, &total);
+    size_t o_surv, o_out, o_t4, o_tc, o_tca, o_sa, total;
+    decode_ws_layout(k, e, blocks, &o_surv, &o_out, &o_t4, &o_tc, &o_tca, &o_sa, &total);
     char* ws = (char*)d_workspace;
     const int rows_pad = rows_pad_for(e);
     if (use_syn_path(k, e, len, pitch, d_src, d_parity, d_out)) {
@@ -865,7 +870,9 @@ int rsgpu_decode_prepare(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch,
                         tcp ? nullptr : (uint4*)(ws + o_t4), tcp ? nullptr : (uint32_t*)(ws + o_tc),
                         (long long)e * rows_pad, tcp ? ctx->d_tc_table : nullptr,
                         tcp ? (unsigned long long*)(ws + o_tca) : nullptr, tc_rows_per_pass(e),
-                        (unsigned long long*)ws, d_status, ctx->stream));
+                        (unsigned long long*)ws, d_status,
+                        tcp && use_fused(ctx, k, e) ? (unsigned long long*)(ws + o_sa) : nullptr,
+                        ctx->stream));
         return RSGPU_OK;
     }
     PrepArgs p{};
@@ -902,8 +909,8 @@ int rsgpu_decode_apply(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch, s
         return RSGPU_OK;
     if (e > k || !d_workspace || !d_status)
         return fail(ctx, RSGPU_ERR_ARG, "rsgpu_decode_apply: bad arguments");
-    size_t o_surv, o_out, o_t4, o_tc, o_tca, total;
-    decode_ws_layout(k, e, blocks, &o_surv, &o_out, &o_t4, &o_tc, &o_tca, &total);
+    size_t o_surv, o_out, o_t4, o_tc, o_tca, o_sa, total;
+    decode_ws_layout(k, e, blocks, &o_surv, &o_out, &o_t4, &o_tc, &o_tca, &o_sa, &total);
     char* ws = (char*)d_workspace;
     const int rows_pad = rows_pad_for(e);
     if (use_syn_path(k, e, len, pitch, d_src, d_parity, d_out)) {
@@ -919,7 +926,8 @@ int rsgpu_decode_apply(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch, s
             RS_HIP(ctx, launch_rs_decode_fused(k, e, d_src, d_parity, d_out, (long long)pitch,
                                                (long long)len, (long long)blocks,
                                                (const uint64_t*)ws,
-                                               (const unsigned long long*)(ws + o_tca), d_status,
+                                               (const unsigned long long*)(ws + o_tca),
+                                               (const unsigned long long*)(ws + o_sa), d_status,
                                                ctx->stream));
             return RSGPU_OK;
         }

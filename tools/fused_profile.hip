@@ -55,12 +55,18 @@ int main(int argc, char** argv)
         v = q[0] + (unsigned long long)(rng() & 255) * tc_handler_stride();
     (void)hipMalloc(&d_addr, addr.size() * 8);
     (void)hipMemcpy(d_addr, addr.data(), addr.size() * 8, hipMemcpyHostToDevice);
+    std::vector<unsigned long long> sa((size_t)B * (k - e) * 32);
+    for (auto& v : sa)
+        v = q[0] + (unsigned long long)(rng() & 255) * tc_handler_stride();
+    unsigned long long* d_sa;
+    (void)hipMalloc(&d_sa, sa.size() * 8);
+    (void)hipMemcpy(d_sa, sa.data(), sa.size() * 8, hipMemcpyHostToDevice);
     (void)hipMalloc(&d_status, B * sizeof(int));
     (void)hipMemset(d_status, 0, B * sizeof(int));
 
     auto run = [&] {
         return launch_rs_decode_fused(k, e, src, par, out, pitch, L, B, (const uint64_t*)d_em,
-                                      d_addr, d_status, 0);
+                                      d_addr, d_sa, d_status, 0);
     };
     (void)run();
     (void)run();
