@@ -57,8 +57,9 @@ def parse():
     p.add_argument("--no-verify", action="store_true")
     p.add_argument("--host-io", type=int, default=0, metavar="BLOCKS",
                    help="also time the host-resident path (H2D + kernel + D2H) on BLOCKS blocks")
-    p.add_argument("--traffic", default=None,
-                   help="JSON with PMC-derived HBM bytes per launch (profiles/)")
+    p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r01_traffic.json"),
+                   help="JSON with PMC-derived HBM bytes per launch of the same workload "
+                        "(tools/profile_round.sh; default: the committed profiles/r01_traffic.json)")
     return p.parse_args()
 
 
@@ -259,9 +260,13 @@ def main():
     dom_ms = tot / n
     dom_bytes = alg.get(dom, 0.0) * nb / n      # algorithmic bytes per launch
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
-    traffic = None
-    if args.traffic and os.path.exists(args.traffic):
+    # PMC bytes per launch come from a separate rocprofv3 --pmc pass of the
+    # same command (counters cannot be read inside this timed run); only
+    # valid for the C3 workload they were measured on
+    traffic, traffic_src = None, None
+    if args.traffic and os.path.exists(args.traffic) and args.config == "c3" and not args.blocks:
         traffic = json.load(open(args.traffic)).get(dom)
+        traffic_src = os.path.relpath(args.traffic, ROOT) if traffic is not None else None
     step_frac = (2 * op_bytes) / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBPS
 
     line = {
@@ -279,7 +284,7 @@ def main():
         "verified": ok,
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
+                     "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic, "traffic_source": traffic_src,
                      "alg_bytes_per_launch": dom_bytes, "avg_ms": round(dom_ms, 3)},
         "cpu_baseline": None,
     }
