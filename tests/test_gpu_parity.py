@@ -203,6 +203,24 @@ def test_benchmark_sizes_round_trip(ctx, orc, k, e, L, B):
     assert dec.err_host[blk].tolist() == erasure_pattern(seed, blk, k, e).tolist()
 
 
+@pytest.mark.parametrize("k,e,L,B", [(64, 32, 1000000, 256), (100, 20, 1000000, 96)])
+def test_full_occupancy_repeated_round_trips(ctx, k, e, L, B):
+    """Enough blocks to fill every CU with several workgroups, encode + decode
+    repeated back to back with a device verify after each: workgroup-level
+    races (a missing barrier between a phase's last LDS reads and the next
+    phase's writes) only show when co-resident workgroups run out of step,
+    which the small-batch parity tests do not provoke."""
+    seed = 99
+    enc = rsgpu.GpuEncoder(k, L, e, blocks=B, seed=seed, ctx=ctx)
+    dec = rsgpu.GpuDecoder(k, L, e, blocks=B, seed=seed, ctx=ctx)
+    for _ in range(3):
+        enc.encode_all()
+        dec.decode_all(enc)
+        torch.cuda.synchronize()
+        assert dec.is_complete()
+        assert dec.verify_data(enc)
+
+
 def test_decode_matches_oracle_decode_rows(ctx, orc):
     """Decoding also recovers from a parity buffer that was produced by the
     oracle (cross-implementation), and recovers garbage-free bytes."""
