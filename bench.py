@@ -240,7 +240,7 @@ def main():
     alg = {"k_rs_bs(encode)": blk_op, "k_rs_encode_lh": blk_op, "k_dot_generic": blk_op,
            "k_rs_bs(syndrome)": blk_op, "k_dot_generic(decode)": blk_op,
            "k_dot_generic(solve)": 2.0 * e * L, "k_rs_tc(solve)": 2.0 * e * L,
-           "k_rs_decode_fused": blk_op, "k_rs_tc(encode)": blk_op,
+           "k_rs_decode_fused": blk_op, "k_rs_tc(encode)": blk_op, "k_rs_tc(decode)": blk_op,
            "k_decode_prepare": 0.0, "k_decode_prepare_syn": 0.0}
     per = {}
     for name, ms, nb in recs:

@@ -12,8 +12,7 @@ Register contract (must match rs_tc.hip; the kernel limits the compiler to
 v0..v63 with amdgpu_num_vgpr(64), so v64..v127 belong to the asm alone):
     acc slot 0 planes   v[ACC .. ACC+7]  (slot s is reached with
                         s_set_gpr_idx_on 8*s, gpr_idx(SRC0,DST))
-    L[n], n = 1..15     v[L0 + n]
-    H[n], n = 1..15     v[H0 + n]
+    L[n], H[n], n = 1..15   v[reg_l(n)], v[reg_h(n)] (layouts below)
     return address      s[RET:RET+1]
     address banks       s[64:79], s[84:99]; m0 save s80; staged planes v[24:31]
     (all of these are clobbers of the one asm statement per chunk)
@@ -21,13 +20,37 @@ v0..v63 with amdgpu_num_vgpr(64), so v64..v127 belong to the asm alone):
 usage: gen_tc_handlers.py OUT.inc [SYN.inc]
   SYN.inc: compile-time syndrome blocks of the fused decode (rs_decode_fused.hip)
 """
+import os
 import sys
 
 ACC = 64
-L0 = 31
-H0 = 46
 RET = 82
 STRIDE = 72  # 8 x 8-byte VOP3 + s_setpc_b64 (4) + s_nop pad (4)
+
+# Table registers.  "late" layout (default): the 8 single-plane entries
+# L1 L2 L4 L8 H1 H2 H4 H8 are v24..v31, so the next source's planes are read
+# from LDS straight into them (after the current source's dispatch; no
+# staging copies); the 11 composite L entries follow at v32.., then the 11 H.
+# "staged" layout (RSGPU_TC_LAYOUT=staged): L[n] = v[31 + n], H[n] = v[46 + n],
+# planes read one source ahead into v24..v31 and copied in (8 v_mov).
+LAYOUT = os.environ.get("RSGPU_TC_LAYOUT", "late")
+assert LAYOUT in ("late", "staged"), LAYOUT
+_COMPOSITE = [n for n in range(1, 16) if n & (n - 1)]
+
+
+def reg_l(n: int) -> int:
+    if LAYOUT == "staged":
+        return 31 + n
+    return 24 + (n.bit_length() - 1) if n & (n - 1) == 0 else 32 + _COMPOSITE.index(n)
+
+
+def reg_h(n: int) -> int:
+    if LAYOUT == "staged":
+        return 46 + n
+    return 28 + (n.bit_length() - 1) if n & (n - 1) == 0 else 43 + _COMPOSITE.index(n)
+
+
+TABLE_REGS = sorted({reg_l(n) for n in range(1, 16)} | {reg_h(n) for n in range(1, 16)})
 
 
 def gf_mul(a: int, b: int) -> int:
@@ -60,11 +83,11 @@ def handler(c: int) -> list:
         lo, hi = m & 15, m >> 4
         acc = ACC + b
         if lo and hi:
-            ins.append(f"v_bitop3_b32 v{acc}, v{acc}, v{L0 + lo}, v{H0 + hi} bitop3:0x96")
+            ins.append(f"v_bitop3_b32 v{acc}, v{acc}, v{reg_l(lo)}, v{reg_h(hi)} bitop3:0x96")
         elif lo:
-            ins.append(f"v_xor_b32_e64 v{acc}, v{acc}, v{L0 + lo}")
+            ins.append(f"v_xor_b32_e64 v{acc}, v{acc}, v{reg_l(lo)}")
         elif hi:
-            ins.append(f"v_xor_b32_e64 v{acc}, v{acc}, v{H0 + hi}")
+            ins.append(f"v_xor_b32_e64 v{acc}, v{acc}, v{reg_h(hi)}")
         else:  # a nonzero c has an invertible matrix: no zero rows
             raise AssertionError("zero row for nonzero coefficient")
     ins.append(f"s_setpc_b64 s[{RET}:{RET + 1}]")
@@ -72,8 +95,8 @@ def handler(c: int) -> list:
     return ins
 
 
-PLANE_REG = [L0 + 1, L0 + 2, L0 + 4, L0 + 8, H0 + 1, H0 + 2, H0 + 4, H0 + 8]
-STAGE = 24       # v[24:31]: next source's planes, read from LDS one source ahead
+PLANE_REG = [reg_l(1), reg_l(2), reg_l(4), reg_l(8), reg_h(1), reg_h(2), reg_h(4), reg_h(8)]
+STAGE = 24       # v[24:31]: next source's planes (staged layout: read one source ahead)
 BANK = (64, 84)  # s[64:79] / s[84:99]: handler addresses of alternate sources
 SM0 = 80         # m0 save
 C = 8            # sources per LDS chunk (rs_tc.hip)
@@ -98,26 +121,30 @@ def chunk(nt: int) -> list:
         off = "0" if t == 0 else f"%[o{t}]"
         return [f"s_load_dwordx16 s[{bank}:{bank + 15}], %[pa], {off}"]
 
+    late = LAYOUT == "late"
     ins = [f"s_mov_b32 s{SM0}, m0"] + sload(0, BANK[0]) + stage(0)
     for t in range(nt):
         cur, nxt = BANK[t & 1], BANK[(t + 1) & 1]
         ins.append("s_waitcnt lgkmcnt(0)")
-        for a, r in enumerate(PLANE_REG):
-            ins.append(f"v_mov_b32_e32 v{r}, v{STAGE + a}")
+        if not late:
+            for a, r in enumerate(PLANE_REG):
+                ins.append(f"v_mov_b32_e32 v{r}, v{STAGE + a}")
         if t + 1 < nt:
-            ins += sload(t + 1, nxt) + stage(t + 1)
-        for base in (L0, H0):
-            for n in range(1, 16):
-                low = n & -n
-                if n != low:
-                    ins.append(f"v_xor_b32_e32 v{base + n}, v{base + (n ^ low)}, v{base + low}")
+            ins += sload(t + 1, nxt) + ([] if late else stage(t + 1))
+        ins += tables()
         # index mode on once per source; slots switch the index only
-        ins.append("s_set_gpr_idx_on 0, gpr_idx(SRC0,DST)")
-        for slot in range(8):
-            if slot:
-                ins.append(f"s_set_gpr_idx_idx {8 * slot}")
-            ins.append(f"s_swappc_b64 s[{RET}:{RET + 1}], s[{cur + 2 * slot}:{cur + 2 * slot + 1}]")
-        ins.append("s_set_gpr_idx_off")
+        if os.environ.get("RSGPU_TC_FAKE") == "inline":  # timing experiment only: wrong products
+            for slot in range(8):
+                ins += mac_lines(0x53 + 16 * slot, slot)
+        else:
+            ins.append("s_set_gpr_idx_on 0, gpr_idx(SRC0,DST)")
+            for slot in range(8):
+                if slot:
+                    ins.append(f"s_set_gpr_idx_idx {8 * slot}")
+                ins.append(f"s_swappc_b64 s[{RET}:{RET + 1}], s[{cur + 2 * slot}:{cur + 2 * slot + 1}]")
+            ins.append("s_set_gpr_idx_off")
+        if late and t + 1 < nt:  # the planes are free once the dispatch is done
+            ins += stage(t + 1)
     ins += [f"s_mov_b32 m0, s{SM0}", "s_nop 0"]
     return ins
 
@@ -147,21 +174,21 @@ def mac_lines(c: int, slot: int) -> list:
         lo, hi = m & 15, m >> 4
         acc = ACC + 8 * slot + b
         if lo and hi:
-            ins.append(f"v_bitop3_b32 v{acc}, v{acc}, v{L0 + lo}, v{H0 + hi} bitop3:0x96")
+            ins.append(f"v_bitop3_b32 v{acc}, v{acc}, v{reg_l(lo)}, v{reg_h(hi)} bitop3:0x96")
         elif lo:
-            ins.append(f"v_xor_b32_e32 v{acc}, v{L0 + lo}, v{acc}")
+            ins.append(f"v_xor_b32_e32 v{acc}, v{reg_l(lo)}, v{acc}")
         elif hi:
-            ins.append(f"v_xor_b32_e32 v{acc}, v{H0 + hi}, v{acc}")
+            ins.append(f"v_xor_b32_e32 v{acc}, v{reg_h(hi)}, v{acc}")
     return ins
 
 
 def tables() -> list:
     ins = []
-    for base in (L0, H0):
+    for reg in (reg_l, reg_h):
         for n in range(1, 16):
             low = n & -n
             if n != low:
-                ins.append(f"v_xor_b32_e32 v{base + n}, v{base + (n ^ low)}, v{base + low}")
+                ins.append(f"v_xor_b32_e32 v{reg(n)}, v{reg(n ^ low)}, v{reg(low)}")
     return ins
 
 
@@ -243,7 +270,7 @@ def write_syn(path: str) -> None:
     """C++ specializations SynBlock<K,E,G,T> / SynTwiddle<K,E,G> / XorSlot<S>
     wrapping the generated asm (rs_decode_fused.hip declares the primaries)."""
     out = ["// generated by gen_tc_handlers.py -- do not edit"]
-    tab = [r for r in list(range(L0 + 1, L0 + 16)) + list(range(H0 + 1, H0 + 16)) if r not in PLANE_REG]
+    tab = [r for r in TABLE_REGS if r not in PLANE_REG]
     clob = ", ".join([f'"v{r}"' for r in tab] + [f'"v{ACC + i}"' for i in range(64)])
     plane_ops = ", ".join(f'"{{v{r}}}"(P[{a}])' for a, r in enumerate(PLANE_REG))
     tw_clob = ", ".join([f'"v{r}"' for r in range(32, 40)] + [f'"v{ACC + i}"' for i in range(64)])
@@ -292,8 +319,7 @@ def main() -> None:
         "// generated by gen_tc_handlers.py -- do not edit",
         f"#define RSGPU_TC_STRIDE {STRIDE}",
         f"#define RSGPU_TC_ACC {ACC}",
-        f"#define RSGPU_TC_L0 {L0}",
-        f"#define RSGPU_TC_H0 {H0}",
+        f"#define RSGPU_TC_LAYOUT_{LAYOUT.upper()} 1",
         f"#define RSGPU_TC_RET {RET}",
         "#define RSGPU_TC_HANDLERS \\",
     ]
@@ -324,7 +350,7 @@ def main() -> None:
         lines.append(f'#define RSGPU_TC_LOAD_SLOT{slot} "global_load_dwordx4 v[{a0}:{a0 + 3}], %0, off\\n'
                      f'global_load_dwordx4 v[{a0 + 4}:{a0 + 7}], %0, off offset:16\\n"')
     lines.append("#define RSGPU_TC_ACC_CLOBBERS " + ", ".join(f'"v{ACC + i}"' for i in range(64)))
-    vclob = list(range(STAGE, STAGE + 8)) + list(range(L0 + 1, L0 + 16)) + list(range(H0 + 1, H0 + 16))
+    vclob = sorted(set(range(STAGE, STAGE + 8)) | set(TABLE_REGS))
     sclob = list(range(BANK[0], BANK[0] + 16)) + [SM0, RET, RET + 1] + list(range(BANK[1], BANK[1] + 16))
     lines.append("#define RSGPU_TC_CLOBBERS " + ", ".join(
         [f'"v{r}"' for r in vclob] + [f'"s{r}"' for r in sclob] + ['"scc"']))

@@ -60,6 +60,10 @@ hipError_t launch_rs_bitsliced(int k, int e, const uint8_t* src, const uint8_t* 
 // handler addresses).  syn_addr (non-null with tc_table): [B][k-e][tc_rows]
 // handler addresses of the syndrome rows 2^(r j) per surviving original j
 // (ascending), for the fused decode's threaded-code syndrome phase.
+// dir_addr (non-null with tc_table): the one-matrix decode through k_rs_tc --
+// srcs [B][k] = surviving originals (ascending) then the e parity rows (from
+// src / par), dsts [B][e] = out rows, dir_addr [B][k][tc_rows] = handler
+// addresses of the e x k decode rows V_E^-1 [V_kept | I].
 hipError_t launch_decode_prepare_syn(int k, int e, int rows_pad, long long blocks,
                                      const uint8_t* err, uint8_t* out, long long out_pitch,
                                      const uint8_t** srcs, uint8_t** dsts, uint4* tabs4,
@@ -67,7 +71,9 @@ hipError_t launch_decode_prepare_syn(int k, int e, int rows_pad, long long block
                                      const unsigned long long* tc_table,
                                      unsigned long long* tc_addr, int tc_rows,
                                      unsigned long long* emask, int* status,
-                                     unsigned long long* syn_addr, hipStream_t st);
+                                     unsigned long long* syn_addr, const uint8_t* src,
+                                     const uint8_t* par, unsigned long long* dir_addr,
+                                     hipStream_t st);
 
 // Threaded-code bit-sliced dot product with runtime coefficients (rs_tc.hip):
 // dsts[b][i] = sum_p c_b[i][p] * srcs[b][p] for rows <= 32, where the

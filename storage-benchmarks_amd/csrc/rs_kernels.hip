@@ -821,7 +821,9 @@ __global__ __launch_bounds__(256) void k_decode_prepare_syn(int k, int e, int ro
                                                             const unsigned long long* tc_table,
                                                             unsigned long long* tc_addr, int tc_rows,
                                                             unsigned long long* emask, int* status,
-                                                            unsigned long long* syn_addr)
+                                                            unsigned long long* syn_addr,
+                                                            const uint8_t* src, const uint8_t* par,
+                                                            unsigned long long* dir_addr)
 {
     extern __shared__ __align__(16) uint8_t lds[];
     uint8_t* gexp = lds;          // 512
@@ -937,13 +939,59 @@ __global__ __launch_bounds__(256) void k_decode_prepare_syn(int k, int e, int ro
     const int st = sh[0];
     if (tid == 0)
         status[b] = st;
-    for (int i = tid; i < e; i += nt) {
-        uint8_t* row = out + ((size_t)b * e + i) * out_pitch;
-        srcs[(size_t)b * e + i] = row;
-        dsts[(size_t)b * e + i] = row;
+    if (!dir_addr) {
+        for (int i = tid; i < e; i += nt) {
+            uint8_t* row = out + ((size_t)b * e + i) * out_pitch;
+            srcs[(size_t)b * e + i] = row;
+            dsts[(size_t)b * e + i] = row;
+        }
     }
     if (st != 0)
         return;
+    if (dir_addr && tc_table) {
+        // One-matrix decode through k_rs_tc: sources = the k - e surviving
+        // originals (ascending) then the e parity rows, outputs = the erased
+        // originals.  d_E = V_E^-1 (P ^ V_kept d_kept), so the coefficient of
+        // survivor q (original lv[q]) for output i is
+        //   sum_p (V_E^-1)[i][p] 2^(p lv[q])   (gf_gen_rs_matrix rows k + p,
+        // isa/ec_base.c:71-78), and of parity row p it is (V_E^-1)[i][p]:
+        // the rows of inv(b) that isa.cpp:177-209 applies (the unique
+        // solution, so bit-exact with the reference's decode).
+        uint8_t* lv = Dm + e * e;  // live list, k - e bytes
+        for (int j = tid; j < k; j += nt) {
+            int below = 0;  // erased originals < j (the list is validated ascending)
+            bool er = false;
+            for (int i = 0; i < e; ++i) {
+                below += eb[i] < j;
+                er |= eb[i] == j;
+            }
+            if (!er)
+                lv[j - below] = (uint8_t)j;
+        }
+        __syncthreads();
+        const int nl = k - e;
+        for (int q = tid; q < k; q += nt)
+            srcs[(size_t)b * k + q] = q < nl ? src + ((size_t)b * k + lv[q]) * out_pitch
+                                             : par + ((size_t)b * e + (q - nl)) * out_pitch;
+        for (int i = tid; i < e; i += nt)
+            dsts[(size_t)b * e + i] = out + ((size_t)b * e + i) * out_pitch;
+        unsigned long long* da = dir_addr + (size_t)b * k * tc_rows;
+        for (int idx = tid; idx < k * tc_rows; idx += nt) {
+            const int q = idx / tc_rows, i = idx - q * tc_rows;
+            uint8_t c = 0;
+            if (i < e) {
+                if (q < nl) {
+                    const int j = lv[q];
+                    for (int p = 0; p < e; ++p)
+                        c ^= gmul(Dm[i * n + p], gexp[(p * j) % 255]);
+                } else {
+                    c = Dm[i * n + (q - nl)];
+                }
+            }
+            da[idx] = tc_table[c];
+        }
+        return;
+    }
     if (syn_addr && tc_table) {
         // syndrome phase of the fused decode (threaded code): the q-th
         // surviving original j_q (ascending) carries coefficient 2^(r j_q)
@@ -1014,7 +1062,9 @@ hipError_t launch_decode_prepare_syn(int k, int e, int rows_pad, long long block
                                      const unsigned long long* tc_table,
                                      unsigned long long* tc_addr, int tc_rows,
                                      unsigned long long* emask, int* status,
-                                     unsigned long long* syn_addr, hipStream_t st)
+                                     unsigned long long* syn_addr, const uint8_t* src,
+                                     const uint8_t* par, unsigned long long* dir_addr,
+                                     hipStream_t st)
 {
     static bool attr_set = false;
     if (!attr_set) {
@@ -1025,7 +1075,7 @@ hipError_t launch_decode_prepare_syn(int k, int e, int rows_pad, long long block
     hipLaunchKernelGGL(k_decode_prepare_syn, dim3((unsigned)blocks), dim3(256),
                        decode_prepare_syn_lds_bytes(e), st, k, e, rows_pad, err, out, out_pitch,
                        srcs, dsts, tabs4, ctab, tab_block_stride, tc_table, tc_addr, tc_rows,
-                       emask, status, syn_addr);
+                       emask, status, syn_addr, src, par, dir_addr);
     return hipGetLastError();
 }
 

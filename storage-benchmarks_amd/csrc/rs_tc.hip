@@ -43,6 +43,7 @@ namespace tc {
 
 using bs::barrier_lds;
 using bs::glds16;
+using bs::glds32;
 using bs::sload_ptr;
 using bs::store32;
 using bs::wait_vm;
@@ -167,11 +168,21 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_num_vgpr(64))) void 
         const long long loff = off + 32 <= a.len ? off : 0;  // out-of-range lanes re-read the row head
         const int c0 = ch * C, nt = min(C, k - c0);
         const uint32_t base = lds0 + (uint32_t)((n & 1) * C * 2 * 64 * 16);
-        for (int t = wave; t < nt; t += NW) {
-            const uint8_t* row = sload_ptr(srcs + c0 + t) + loff;
-            glds16(row, base + (uint32_t)((t * 2 + 0) * 64 * 16));
-            glds16(row + 16, base + (uint32_t)((t * 2 + 1) * 64 * 16));
+        // this wave's row pointers of the chunk, two scalar loads under one
+        // wait when it owns two sources (load and wait in ONE asm statement:
+        // the compiler must not see an output before it has landed)
+        int t = wave;
+        for (; t + NW < nt; t += 2 * NW) {
+            const uint8_t *r0, *r1;
+            asm volatile("s_load_dwordx2 %0, %2, 0\n s_load_dwordx2 %1, %3, 0\n s_waitcnt lgkmcnt(0)"
+                         : "=&s"(r0), "=&s"(r1)
+                         : "s"(srcs + c0 + t), "s"(srcs + c0 + t + NW)
+                         : "memory");
+            glds32(r0, (uint32_t)loff, base + (uint32_t)(t * 2 * 64 * 16));
+            glds32(r1, (uint32_t)loff, base + (uint32_t)((t + NW) * 2 * 64 * 16));
         }
+        if (t < nt)
+            glds32(sload_ptr(srcs + c0 + t), (uint32_t)loff, base + (uint32_t)(t * 2 * 64 * 16));
     };
 
     TC_PROF_DECL

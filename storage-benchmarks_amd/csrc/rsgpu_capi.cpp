@@ -791,16 +791,35 @@ static bool use_tc(rsgpu_ctx* ctx, int e)
     return tc_init(ctx) == 1;
 }
 
-// The one-pass fused decode (RSGPU_NO_FUSED=1 selects the two-kernel
-// syndrome + solve path instead, for comparison).
-static bool use_fused(rsgpu_ctx*, int k, int e)
+// Decode kernels of the syndrome path once threaded code is available
+// (RSGPU_DECODE, read once per process):
+//   direct (default)  one matrix: k_rs_tc over the k - e survivors and the e
+//                     parity rows with the e x k decode rows (one pass, HBM
+//                     traffic (k + e) L per block)
+//   fused             k_rs_decode_fused: syndromes + e x e solve per tile
+//                     (instantiated codes only)
+//   split             k_rs_bs syndromes to HBM, then the in-place k_rs_tc solve
+// RSGPU_NO_FUSED=1 (older switch) means split.
+enum class DecodeMode { direct, fused, split };
+
+static DecodeMode decode_mode(int k, int e)
 {
-    static const bool off = [] {
-        const char* v = std::getenv("RSGPU_NO_FUSED");
-        return v && v[0] == '1';
+    static const DecodeMode m = [] {
+        const char* v = std::getenv("RSGPU_DECODE");
+        const char* nf = std::getenv("RSGPU_NO_FUSED");
+        if (v && std::strcmp(v, "fused") == 0)
+            return DecodeMode::fused;
+        if ((v && std::strcmp(v, "split") == 0) || (nf && nf[0] == '1'))
+            return DecodeMode::split;
+        return DecodeMode::direct;
     }();
-    return !off && rs_decode_fused_available(k, e);
+    if (m == DecodeMode::fused && !rs_decode_fused_available(k, e))
+        return DecodeMode::split;
+    return m;
 }
+
+static bool use_fused(rsgpu_ctx*, int k, int e) { return decode_mode(k, e) == DecodeMode::fused; }
+static bool use_direct(rsgpu_ctx*, int k, int e) { return decode_mode(k, e) == DecodeMode::direct; }
 
 // Syndrome decode (bit-sliced syndromes + runtime e x e in place) applies to
 // the instantiated codes with 32-byte-multiple rows; otherwise the direct
@@ -827,7 +846,10 @@ static void decode_ws_layout(int k, int e, size_t blocks, size_t* off_surv, size
     o = align_up(o + sizeof(uint4) * (size_t)k * rows_pad * blocks, 256);
     *off_tc = o;
     o = align_up(o + sizeof(uint32_t) * (size_t)k * rows_pad * blocks, 256);
-    *off_tca = o;  // k_rs_tc handler addresses [blocks][e][tc_rows]
+    // k_rs_tc handler addresses: [blocks][e][tc_rows] (split / fused solve)
+    // or, for the one-matrix decode, [blocks][k][tc_rows] spanning this
+    // region and the next one
+    *off_tca = o;
     o = align_up(o + sizeof(unsigned long long) * (size_t)e * tc_rows_per_pass(e) * blocks, 256);
     *off_sa = o;  // fused decode: syndrome-phase handler addresses [blocks][k-e][tc_rows]
     o = align_up(o + sizeof(unsigned long long) * (size_t)(k > e ? k - e : 0) * tc_rows_per_pass(e) *
@@ -872,6 +894,8 @@ int rsgpu_decode_prepare(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch,
                         tcp ? (unsigned long long*)(ws + o_tca) : nullptr, tc_rows_per_pass(e),
                         (unsigned long long*)ws, d_status,
                         tcp && use_fused(ctx, k, e) ? (unsigned long long*)(ws + o_sa) : nullptr,
+                        d_src, d_parity,
+                        tcp && use_direct(ctx, k, e) ? (unsigned long long*)(ws + o_tca) : nullptr,
                         ctx->stream));
         return RSGPU_OK;
     }
@@ -920,6 +944,21 @@ int rsgpu_decode_apply(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch, s
         // on two streams so that the syndromes of chunk i+1 overlap the solve
         // of chunk i.
         const bool tcp = use_tc(ctx, e);
+        if (tcp && use_direct(ctx, k, e)) {
+            // one pass, one matrix (prepared by k_decode_prepare_syn)
+            TcArgs t{};
+            t.srcs = (const uint8_t* const*)(ws + o_surv);
+            t.dsts = (uint8_t* const*)(ws + o_out);
+            t.addr = (const unsigned long long*)(ws + o_tca);
+            t.addr_stride = (long long)k * tc_rows_per_pass(e);
+            t.k = k;
+            t.rows = e;
+            t.len = (long long)len;
+            t.status = d_status;
+            KTimer kt(ctx, "k_rs_tc(decode)", blocks);
+            RS_HIP(ctx, launch_rs_tc(t, (long long)blocks, ctx->stream));
+            return RSGPU_OK;
+        }
         if (tcp && use_fused(ctx, k, e)) {
             // one pass: syndromes + solve per column tile (rs_decode_fused.hip)
             KTimer kt(ctx, "k_rs_decode_fused", blocks);

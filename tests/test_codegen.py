@@ -122,3 +122,71 @@ def test_syndrome_blocks_horner(plan):
                 exp = [x ^ g.gf_mul(cj, y) for x, y in zip(exp, data[j])]
             got = unplanes([regs[g.ACC + 8 * s + a] for a in range(8)])
             assert got == exp, (plan, r)
+
+
+DS = re.compile(r"ds_read_b128 v\[(\d+):(\d+)\], %\[la\] offset:(\d+)")
+SLD = re.compile(r"s_load_dwordx16 s\[(\d+):(\d+)\], %\[pa\], (\S+)")
+SWAP = re.compile(r"s_swappc_b64 s\[\d+:\d+\], s\[(\d+):\d+\]")
+
+
+@pytest.mark.parametrize("nt", range(1, g.C + 1))
+def test_chunk_dispatch(nt):
+    """The per-part chunk asm (gen_tc_handlers.chunk) interpreted with its
+    LDS reads, handler-address loads, GPR-index relocation and handler calls:
+    every accumulator slot s must end as acc_s ^ sum_t c(t, s) * src_t.  The
+    interpreter applies each load at issue, so a read that lands in a register
+    still in use by the dispatch shows up as a wrong product."""
+    rng = random.Random(100 + nt)
+    src = [[rng.randrange(256) for _ in range(32)] for _ in range(nt)]
+    coef = [[rng.randrange(256) for _ in range(8)] for _ in range(nt)]
+    acc0 = [[rng.randrange(256) for _ in range(32)] for _ in range(8)]
+    regs = {i: 0 for i in range(256)}
+    for s in range(8):
+        for a, v in enumerate(planes(acc0[s])):
+            regs[g.ACC + 8 * s + a] = v
+    sregs, idx = {}, None
+    for i in g.chunk(nt):
+        m = DS.match(i)
+        if m:
+            lo, hi, off = int(m.group(1)), int(m.group(2)), int(m.group(3))
+            t, half = off // g.LDS_T, (off % g.LDS_T) // g.LDS_H
+            p = planes(src[t])
+            for q in range(hi - lo + 1):
+                regs[lo + q] = p[4 * half + q]
+            continue
+        m = SLD.match(i)
+        if m:
+            base, off = int(m.group(1)), m.group(3)
+            t = 0 if off == "0" else int(off[3:-1])
+            for s in range(8):
+                sregs[base + 2 * s] = coef[t][s]
+            continue
+        if i.startswith("s_set_gpr_idx_on"):
+            idx = 0
+        elif i.startswith("s_set_gpr_idx_idx"):
+            idx = int(i.split()[1])
+        elif i.startswith("s_set_gpr_idx_off"):
+            idx = None
+        elif i.startswith("s_swappc"):
+            assert idx is not None
+            c = sregs[int(SWAP.match(i).group(1))]
+            for h in g.handler(c):
+                if h.startswith("s_"):
+                    continue
+                mm = INSN.match(h)
+                op, d = mm.group(1), int(mm.group(2)) + idx
+                ops = [int(x) for x in mm.groups()[2:] if x]
+                ops[0] += idx  # gpr_idx(SRC0,DST)
+                val = 0
+                for o in ops:
+                    val ^= regs[o]
+                assert op.startswith(("v_xor", "v_bitop3"))
+                regs[d] = val
+        elif not i.startswith("s_"):
+            assert idx is None, i
+            run([i], regs)
+    for s in range(8):
+        exp = list(acc0[s])
+        for t in range(nt):
+            exp = [x ^ g.gf_mul(coef[t][s], y) for x, y in zip(exp, src[t])]
+        assert unplanes([regs[g.ACC + 8 * s + a] for a in range(8)]) == exp, (nt, s)

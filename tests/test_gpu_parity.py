@@ -290,6 +290,22 @@ def test_plugin_dropin_reference_shape():
     assert r.stdout.count("complete=1 verified=1") == 6, r.stdout
 
 
+@pytest.mark.parametrize("mode", ["fused", "split", "direct"])
+def test_decode_modes_end_to_end(mode):
+    """Every decode kernel choice of the syndrome path (RSGPU_DECODE, read
+    once per process -- hence a child process per mode): the one-matrix
+    k_rs_tc decode (default), the fused syndrome + solve kernel, and the
+    split syndrome kernel + in-place solve, through the reference-shaped
+    plugin with device verification of every recovered byte."""
+    import subprocess
+    exe = os.path.join(os.path.dirname(HERE), "storage-benchmarks_amd", "bin", "plugin_dropin_test")
+    env = dict(os.environ, RSGPU_DECODE=mode)
+    r = subprocess.run([exe, "16:64000:8", "64:1000000:32", "100:64000:20", "64:32000:32", "20:4096:7"],
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert r.stdout.count("complete=1 verified=1") == 5, r.stdout
+
+
 @pytest.mark.parametrize("k,e,L,B,kind", [
     (32, 8, 4096, 3, "all256"),   # coefficient (r*32 + j) & 255: every value 0..255 once
     (13, 20, 2048, 2, "random"),  # partial LDS chunks (13 = 8 + 5), 3 wave groups
