@@ -73,15 +73,29 @@ def mat_row(c: int, b: int) -> int:
     return row
 
 
-def handler(c: int) -> list:
+# Chained dispatch (default; RSGPU_TC_CHAIN=0 for call/return per slot): a
+# second copy of the handlers serves the odd slot of each slot pair.  An even
+# handler works on slot 2p (v[ACC..] relocated by 16p) and jumps straight to
+# the odd handler whose address the chunk put in s[RA:RA+1]; the odd handler
+# works on slot 2p+1 (v[ACC+8..], same relocation) and returns.  Three jumps
+# and five SALU per slot pair instead of four and six.
+CHAIN = os.environ.get("RSGPU_TC_CHAIN", "1") == "1"
+NHANDLERS = 512 if CHAIN else 256
+RA = 100
+
+
+def handler(c: int, odd: bool = False) -> list:
+    """Handler of coefficient c; `odd` = the odd-slot copy of chained mode."""
+    ret = RA if CHAIN and not odd else RET
+    base = ACC + 8 if CHAIN and odd else ACC
     if c == 0:
-        # no-op: return at once; pad to STRIDE with never-executed s_nop
-        return [f"s_setpc_b64 s[{RET}:{RET + 1}]"] + ["s_nop 0"] * ((STRIDE - 4) // 4)
+        # no-op: continue at once; pad to STRIDE with never-executed s_nop
+        return [f"s_setpc_b64 s[{ret}:{ret + 1}]"] + ["s_nop 0"] * ((STRIDE - 4) // 4)
     ins = []
     for b in range(8):
         m = mat_row(c, b)
         lo, hi = m & 15, m >> 4
-        acc = ACC + b
+        acc = base + b
         if lo and hi:
             ins.append(f"v_bitop3_b32 v{acc}, v{acc}, v{reg_l(lo)}, v{reg_h(hi)} bitop3:0x96")
         elif lo:
@@ -90,9 +104,16 @@ def handler(c: int) -> list:
             ins.append(f"v_xor_b32_e64 v{acc}, v{acc}, v{reg_h(hi)}")
         else:  # a nonzero c has an invertible matrix: no zero rows
             raise AssertionError("zero row for nonzero coefficient")
-    ins.append(f"s_setpc_b64 s[{RET}:{RET + 1}]")
+    ins.append(f"s_setpc_b64 s[{ret}:{ret + 1}]")
     ins.append("s_nop 0")
     return ins
+
+
+def handler_table() -> list:
+    """All handlers in address order: c = 0..255 (even / only copy), then in
+    chained mode the odd copy.  Handler number h lives at base + h * STRIDE."""
+    return [i for odd in ((False, True) if CHAIN else (False,)) for c in range(256)
+            for i in handler(c, odd)]
 
 
 PLANE_REG = [reg_l(1), reg_l(2), reg_l(4), reg_l(8), reg_h(1), reg_h(2), reg_h(4), reg_h(8)]
@@ -136,6 +157,14 @@ def chunk(nt: int) -> list:
         if os.environ.get("RSGPU_TC_FAKE") == "inline":  # timing experiment only: wrong products
             for slot in range(8):
                 ins += mac_lines(0x53 + 16 * slot, slot)
+        elif CHAIN:
+            ins.append("s_set_gpr_idx_on 0, gpr_idx(SRC0,DST)")
+            for p in range(4):
+                if p:
+                    ins.append(f"s_set_gpr_idx_idx {16 * p}")
+                ins.append(f"s_mov_b64 s[{RA}:{RA + 1}], s[{cur + 4 * p + 2}:{cur + 4 * p + 3}]")
+                ins.append(f"s_swappc_b64 s[{RET}:{RET + 1}], s[{cur + 4 * p}:{cur + 4 * p + 1}]")
+            ins.append("s_set_gpr_idx_off")
         else:
             ins.append("s_set_gpr_idx_on 0, gpr_idx(SRC0,DST)")
             for slot in range(8):
@@ -320,12 +349,12 @@ def main() -> None:
         f"#define RSGPU_TC_STRIDE {STRIDE}",
         f"#define RSGPU_TC_ACC {ACC}",
         f"#define RSGPU_TC_LAYOUT_{LAYOUT.upper()} 1",
+        f"#define RSGPU_TC_NHANDLERS {NHANDLERS}",
         f"#define RSGPU_TC_RET {RET}",
         "#define RSGPU_TC_HANDLERS \\",
     ]
-    for c in range(256):
-        for i in handler(c):
-            lines.append(f'    "{i}\\n" \\')
+    for i in handler_table():
+        lines.append(f'    "{i}\\n" \\')
     lines.append("")
     for nt in range(1, C + 1):
         lines.append(f"#define RSGPU_TC_CHUNK{nt} \\")
@@ -352,6 +381,8 @@ def main() -> None:
     lines.append("#define RSGPU_TC_ACC_CLOBBERS " + ", ".join(f'"v{ACC + i}"' for i in range(64)))
     vclob = sorted(set(range(STAGE, STAGE + 8)) | set(TABLE_REGS))
     sclob = list(range(BANK[0], BANK[0] + 16)) + [SM0, RET, RET + 1] + list(range(BANK[1], BANK[1] + 16))
+    if CHAIN:
+        sclob += [RA, RA + 1]
     lines.append("#define RSGPU_TC_CLOBBERS " + ", ".join(
         [f'"v{r}"' for r in vclob] + [f'"s{r}"' for r in sclob] + ['"scc"']))
     lines.append("")

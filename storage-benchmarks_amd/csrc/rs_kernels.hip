@@ -988,7 +988,7 @@ __global__ __launch_bounds__(256) void k_decode_prepare_syn(int k, int e, int ro
                     c = Dm[i * n + (q - nl)];
                 }
             }
-            da[idx] = tc_table[c];
+            da[idx] = tc_table[(i & 1) * 256 + c];
         }
         return;
     }
@@ -1012,7 +1012,7 @@ __global__ __launch_bounds__(256) void k_decode_prepare_syn(int k, int e, int ro
         unsigned long long* sa = syn_addr + (size_t)b * (k - e) * tc_rows;
         for (int idx = tid; idx < (k - e) * tc_rows; idx += nt) {
             const int q = idx / tc_rows, r = idx - q * tc_rows;
-            sa[idx] = tc_table[r < e ? gexp[(r * (int)lv[q]) % 255] : 0];
+            sa[idx] = tc_table[(r & 1) * 256 + (r < e ? gexp[(r * (int)lv[q]) % 255] : 0)];
         }
     }
     if (tc_addr) {
@@ -1021,7 +1021,7 @@ __global__ __launch_bounds__(256) void k_decode_prepare_syn(int k, int e, int ro
         unsigned long long* ta = tc_addr + (size_t)b * e * tc_rows;
         for (int idx = tid; idx < e * tc_rows; idx += nt) {
             const int p = idx / tc_rows, i = idx - p * tc_rows;
-            ta[idx] = tc_table[i < e ? Dm[i * n + p] : 0];
+            ta[idx] = tc_table[(i & 1) * 256 + (i < e ? Dm[i * n + p] : 0)];
         }
     }
     if (!tabs4)

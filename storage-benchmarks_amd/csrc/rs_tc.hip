@@ -275,6 +275,8 @@ hipError_t tc_query_handlers(unsigned long long* d_out, hipStream_t st)
 
 int tc_handler_stride() { return RSGPU_TC_STRIDE; }
 
+int tc_handler_count() { return RSGPU_TC_NHANDLERS; }
+
 int tc_rows_per_pass(int rows) { return rows <= 0 ? 8 : (rows + 7) / 8 * 8; }
 
 hipError_t launch_rs_tc(const TcArgs& a, long long blocks, hipStream_t st)

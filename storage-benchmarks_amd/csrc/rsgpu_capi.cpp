@@ -27,7 +27,7 @@ struct rsgpu_ctx {
     // threaded-code solve (rs_tc.hip): device table of the 256 handler
     // addresses; tc_state 0 = not probed, 1 = ready, -1 = unavailable
     unsigned long long* d_tc_table = nullptr;
-    unsigned long long h_tc_table[256] = {};
+    unsigned long long h_tc_table[512] = {};  // [slot parity][coefficient]
     int tc_state = 0;
     std::string err;
     // grow-only device scratch for pointer tables / coefficient tables
@@ -686,33 +686,35 @@ int rsgpu_encode_blocks(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch, 
 
 // Locate the handler table of k_rs_tc once per context: the query kernel
 // reports the table's first and end addresses; the layout must be exactly
-// 256 handlers of tc_handler_stride() bytes, otherwise the threaded-code path
-// stays off (and k_dot_generic solves).
+// tc_handler_count() handlers of tc_handler_stride() bytes, otherwise the
+// threaded-code path stays off (and k_dot_generic solves).  The address
+// table has 512 entries: [slot parity][coefficient].
 static int tc_init(rsgpu_ctx* ctx)
 {
     if (ctx->tc_state != 0)
         return ctx->tc_state;
     ctx->tc_state = -1;
     unsigned long long* d = nullptr;
-    if (hipMalloc((void**)&d, 258 * sizeof(unsigned long long)) != hipSuccess)
+    if (hipMalloc((void**)&d, 514 * sizeof(unsigned long long)) != hipSuccess)
         return -1;
     unsigned long long se[2] = {0, 0};
-    if (tc_query_handlers(d + 256, ctx->stream) != hipSuccess ||
-        hipMemcpyAsync(se, d + 256, sizeof se, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
+    if (tc_query_handlers(d + 512, ctx->stream) != hipSuccess ||
+        hipMemcpyAsync(se, d + 512, sizeof se, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
         hipStreamSynchronize(ctx->stream) != hipSuccess) {
         (void)hipFree(d);
         return -1;
     }
     const unsigned long long stride = (unsigned long long)tc_handler_stride();
-    if (se[0] == 0 || se[1] - se[0] != 256 * stride) {
+    const unsigned long long count = (unsigned long long)tc_handler_count();
+    if (se[0] == 0 || se[1] - se[0] != count * stride || (count != 256 && count != 512)) {
         std::fprintf(stderr, "rsgpu: threaded-code handler table has an unexpected layout "
                              "(%#llx..%#llx); using k_dot_generic\n", se[0], se[1]);
         (void)hipFree(d);
         return -1;
     }
-    unsigned long long h[256];
-    for (int c = 0; c < 256; ++c)
-        h[c] = se[0] + (unsigned long long)c * stride;
+    unsigned long long h[512];
+    for (int c = 0; c < 512; ++c)
+        h[c] = se[0] + (unsigned long long)(count == 512 ? c : c & 255) * stride;
     if (hipMemcpy(d, h, sizeof h, hipMemcpyHostToDevice) != hipSuccess) {
         (void)hipFree(d);
         return -1;
@@ -735,7 +737,7 @@ void tc_fill_addr(const rsgpu_ctx* ctx, const uint8_t* coef, int k, int rows, un
     const int slots = tc_rows_per_pass(rows);
     for (int j = 0; j < k; ++j)
         for (int s = 0; s < slots; ++s)
-            h[(size_t)j * slots + s] = ctx->h_tc_table[s < rows ? coef[(size_t)s * k + j] : 0];
+            h[(size_t)j * slots + s] = ctx->h_tc_table[(s & 1) * 256 + (s < rows ? coef[(size_t)s * k + j] : 0)];
 }
 
 int tc_launch_shared(rsgpu_ctx* ctx, const unsigned long long* d_addr, int k, int rows, long long len,

@@ -56,18 +56,28 @@ def load_tables(regs, by):
 
 @pytest.mark.parametrize("c", range(256))
 def test_handler_multiplies(c):
-    rng = random.Random(c)
-    regs = {i: 0 for i in range(256)}
-    src = [rng.randrange(256) for _ in range(32)]
-    acc = [rng.randrange(256) for _ in range(32)]
-    load_tables(regs, src)
-    for a, v in enumerate(planes(acc)):
-        regs[g.ACC + a] = v
-    body = g.handler(c)
-    assert sum(4 if i.startswith("s_") else 8 for i in body) == g.STRIDE
-    run(body, regs)
-    got = unplanes([regs[g.ACC + a] for a in range(8)])
-    assert got == [x ^ g.gf_mul(c, y) for x, y in zip(acc, src)]
+    for odd in (False, True):
+        rng = random.Random(c)
+        regs = {i: 0 for i in range(256)}
+        src = [rng.randrange(256) for _ in range(32)]
+        acc = [rng.randrange(256) for _ in range(32)]
+        load_tables(regs, src)
+        base = g.ACC + (8 if g.CHAIN and odd else 0)
+        for a, v in enumerate(planes(acc)):
+            regs[base + a] = v
+        body = g.handler(c, odd)
+        assert sum(4 if i.startswith("s_") else 8 for i in body) == g.STRIDE
+        # even copy of chained mode continues at s[RA], everything else returns
+        ret = g.RA if g.CHAIN and not odd else g.RET
+        assert f"s_setpc_b64 s[{ret}:{ret + 1}]" in body
+        run(body, regs)
+        got = unplanes([regs[base + a] for a in range(8)])
+        assert got == [x ^ g.gf_mul(c, y) for x, y in zip(acc, src)]
+
+
+def test_handler_table_layout():
+    tbl = g.handler_table()
+    assert sum(4 if i.startswith("s_") else 8 for i in tbl) == g.NHANDLERS * g.STRIDE
 
 
 def test_lin_inplace_all_constants():
@@ -127,6 +137,8 @@ def test_syndrome_blocks_horner(plan):
 DS = re.compile(r"ds_read_b128 v\[(\d+):(\d+)\], %\[la\] offset:(\d+)")
 SLD = re.compile(r"s_load_dwordx16 s\[(\d+):(\d+)\], %\[pa\], (\S+)")
 SWAP = re.compile(r"s_swappc_b64 s\[\d+:\d+\], s\[(\d+):\d+\]")
+SMOV = re.compile(r"s_mov_b64 s\[(\d+):\d+\], s\[(\d+):\d+\]")
+SETPC = re.compile(r"s_setpc_b64 s\[(\d+):\d+\]")
 
 
 @pytest.mark.parametrize("nt", range(1, g.C + 1))
@@ -167,21 +179,31 @@ def test_chunk_dispatch(nt):
             idx = int(i.split()[1])
         elif i.startswith("s_set_gpr_idx_off"):
             idx = None
+        elif i.startswith("s_mov_b64"):
+            m = SMOV.match(i)
+            sregs[int(m.group(1))] = sregs[int(m.group(2))]
         elif i.startswith("s_swappc"):
             assert idx is not None
-            c = sregs[int(SWAP.match(i).group(1))]
-            for h in g.handler(c):
-                if h.startswith("s_"):
-                    continue
-                mm = INSN.match(h)
-                op, d = mm.group(1), int(mm.group(2)) + idx
-                ops = [int(x) for x in mm.groups()[2:] if x]
-                ops[0] += idx  # gpr_idx(SRC0,DST)
-                val = 0
-                for o in ops:
-                    val ^= regs[o]
-                assert op.startswith(("v_xor", "v_bitop3"))
-                regs[d] = val
+            c, odd = sregs[int(SWAP.match(i).group(1))], False
+            while True:  # a handler, and in chained mode the one it jumps to
+                body = g.handler(c, odd)
+                for h in body:
+                    if h.startswith("s_"):
+                        continue
+                    mm = INSN.match(h)
+                    op, d = mm.group(1), int(mm.group(2)) + idx
+                    ops = [int(x) for x in mm.groups()[2:] if x]
+                    ops[0] += idx  # gpr_idx(SRC0,DST)
+                    val = 0
+                    for o in ops:
+                        val ^= regs[o]
+                    assert op.startswith(("v_xor", "v_bitop3"))
+                    regs[d] = val
+                tgt = int(SETPC.search(" ".join(body)).group(1))
+                if tgt == g.RET:
+                    break
+                assert g.CHAIN and tgt == g.RA and not odd
+                c, odd = sregs[g.RA], True
         elif not i.startswith("s_"):
             assert idx is None, i
             run([i], regs)
@@ -190,3 +212,4 @@ def test_chunk_dispatch(nt):
         for t in range(nt):
             exp = [x ^ g.gf_mul(coef[t][s], y) for x, y in zip(exp, src[t])]
         assert unplanes([regs[g.ACC + 8 * s + a] for a in range(8)]) == exp, (nt, s)
+

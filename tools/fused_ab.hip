@@ -22,6 +22,10 @@ int main(int argc, char** argv)
     const int B = argc > 1 ? atoi(argv[1]) : 1024;
     const int R = argc > 2 ? atoi(argv[2]) : 7;
     const int k = 64, e = 32;
+    // RSGPU_AB_NC=n: coefficients drawn from 1..n only (instruction-cache
+    // working set experiment; products wrong, timing only)
+    const unsigned nc = std::getenv("RSGPU_AB_NC") ? (unsigned)atoi(std::getenv("RSGPU_AB_NC")) : 255u;
+
     const long long L = 1000000, pitch = 1000192;
     uint8_t *src, *par, *out;
     if (hipMalloc(&src, (size_t)B * k * pitch) != hipSuccess ||
@@ -62,14 +66,15 @@ int main(int argc, char** argv)
     (void)tc_query_handlers(d_q, 0);
     unsigned long long q[2];
     (void)hipMemcpy(q, d_q, 16, hipMemcpyDeviceToHost);
-    if (q[1] - q[0] != 256ull * tc_handler_stride()) {
+    if (q[1] - q[0] != (unsigned long long)tc_handler_count() * tc_handler_stride()) {
         printf("bad handler table\n");
         return 1;
     }
     auto table = [&](size_t n) {
         std::vector<unsigned long long> v(n);
-        for (auto& x : v)
-            x = q[0] + (unsigned long long)(1 + rng() % 255) * tc_handler_stride();
+        for (size_t i = 0; i < n; ++i)  // odd slots: the odd-slot copy when chained
+            v[i] = q[0] + (unsigned long long)((tc_handler_count() == 512 && (i & 1) ? 256 : 0) +
+                                               1 + rng() % nc) * tc_handler_stride();
         unsigned long long* d;
         (void)hipMalloc(&d, n * 8);
         (void)hipMemcpy(d, v.data(), n * 8, hipMemcpyHostToDevice);

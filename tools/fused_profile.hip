@@ -46,18 +46,20 @@ int main(int argc, char** argv)
     (void)tc_query_handlers(d_q, 0);
     unsigned long long q[2];
     (void)hipMemcpy(q, d_q, 16, hipMemcpyDeviceToHost);
-    if (q[1] - q[0] != 256ull * tc_handler_stride()) {
+    if (q[1] - q[0] != (unsigned long long)tc_handler_count() * tc_handler_stride()) {
         printf("bad handler table\n");
         return 1;
     }
     std::vector<unsigned long long> addr((size_t)B * e * 32);
-    for (auto& v : addr)
-        v = q[0] + (unsigned long long)(rng() & 255) * tc_handler_stride();
+    // odd slots use the odd-slot handler copy when the dispatch is chained
+    auto odd = [](size_t i) { return tc_handler_count() == 512 && (i & 1) ? 256ull : 0ull; };
+    for (size_t i = 0; i < addr.size(); ++i)
+        addr[i] = q[0] + (odd(i) + (rng() & 255)) * tc_handler_stride();
     (void)hipMalloc(&d_addr, addr.size() * 8);
     (void)hipMemcpy(d_addr, addr.data(), addr.size() * 8, hipMemcpyHostToDevice);
     std::vector<unsigned long long> sa((size_t)B * (k - e) * 32);
-    for (auto& v : sa)
-        v = q[0] + (unsigned long long)(rng() & 255) * tc_handler_stride();
+    for (size_t i = 0; i < sa.size(); ++i)
+        sa[i] = q[0] + (odd(i) + (rng() & 255)) * tc_handler_stride();
     unsigned long long* d_sa;
     (void)hipMalloc(&d_sa, sa.size() * 8);
     (void)hipMemcpy(d_sa, sa.data(), sa.size() * 8, hipMemcpyHostToDevice);

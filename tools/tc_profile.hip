@@ -35,16 +35,17 @@ int main(int argc, char** argv)
     (void)tc_query_handlers(d_q, 0);
     unsigned long long q[2];
     (void)hipMemcpy(q, d_q, 16, hipMemcpyDeviceToHost);
-    if (q[1] - q[0] != 256ull * tc_handler_stride()) {
+    if (q[1] - q[0] != (unsigned long long)tc_handler_count() * tc_handler_stride()) {
         printf("bad handler table\n");
         return 1;
     }
     const int slots = tc_rows_per_pass(k);
     std::vector<unsigned long long> addr((size_t)B * k * slots);
     uint32_t x = 12345;
-    for (auto& v : addr) {
+    for (size_t i = 0; i < addr.size(); ++i) {  // odd slots: odd-slot copy when chained
         x = x * 1664525u + 1013904223u;
-        v = q[0] + (unsigned long long)((x >> 13) & 255) * tc_handler_stride();
+        const unsigned long long h = (tc_handler_count() == 512 && (i & 1) ? 256 : 0) + ((x >> 13) & 255);
+        addr[i] = q[0] + h * tc_handler_stride();
     }
     unsigned long long* d_addr;
     (void)hipMalloc(&d_addr, addr.size() * 8);
