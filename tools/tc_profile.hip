@@ -16,6 +16,7 @@ int main(int argc, char** argv)
     using namespace rsgpu;
     const int B = argc > 1 ? atoi(argv[1]) : 256;
     const int k = argc > 2 ? atoi(argv[2]) : 32;
+    const int nrows = argc > 3 ? atoi(argv[3]) : k;  // output rows (the C3 decode: k 64, rows 32)
     const long long L = 1000000, pitch = 1000192;
     uint8_t* rows;
     if (hipMalloc(&rows, (size_t)B * k * pitch) != hipSuccess) {
@@ -39,7 +40,7 @@ int main(int argc, char** argv)
         printf("bad handler table\n");
         return 1;
     }
-    const int slots = tc_rows_per_pass(k);
+    const int slots = tc_rows_per_pass(nrows);
     std::vector<unsigned long long> addr((size_t)B * k * slots);
     uint32_t x = 12345;
     for (size_t i = 0; i < addr.size(); ++i) {  // odd slots: odd-slot copy when chained
@@ -56,7 +57,8 @@ int main(int argc, char** argv)
     a.dsts = (uint8_t* const*)d_ptr;
     a.addr = d_addr;
     a.k = k;
-    a.rows = k;
+    a.rows = nrows;
+    a.addr_stride = (long long)k * slots;
     a.len = L;
     a.status = nullptr;
     for (int i = 0; i < 2; ++i)
@@ -77,8 +79,8 @@ int main(int argc, char** argv)
     const double waves = (double)(((L + 2047) / 2048 + 63) / 64) * B * (slots / 8);  // sampled WGs
     const char* names[8] = {"issue DMA", "wait vmcnt", "transpose in", "barrier 1",
                             "chunk asm", "store out", "barrier 2 + loop", "wave lifetime"};
-    printf("k_rs_tc<%d>: B=%d k=%d L=%lld  %.3f ms  (%.1f GB/s alg)\n", slots / 8, B, k, L, ms,
-           2.0 * k * L * B / (ms * 1e-3) / 1e9);
+    printf("k_rs_tc<%d>: B=%d k=%d rows=%d L=%lld  %.3f ms  (%.1f GB/s alg)\n", slots / 8, B, k, nrows,
+           L, ms, (double)(k + nrows) * L * B / (ms * 1e-3) / 1e9);
     for (int i = 0; i < 8; ++i)
         printf("  %-18s %10.0f cycles/wave  %5.1f %%\n", names[i], prof[i] / waves,
                100.0 * prof[i] / prof[7]);
