@@ -27,8 +27,13 @@ struct PrepArgs {
     uint8_t* out; long long out_pitch;
     const uint8_t** surv_ptrs;    // device [blocks][k]
     uint8_t** out_ptrs;           // device [blocks][e]
-    uint4* tabs4; uint32_t* ctab; long long tab_block_stride;
+    uint4* tabs4; uint32_t* ctab; long long tab_block_stride;  // v_perm tables, or nullptr
     int* status;                  // device [blocks]
+    // k_rs_tc instead of k_dot_generic (when non-null): the context's
+    // 512-entry handler table and the [blocks][k][tc_rows] address output
+    const unsigned long long* tc_table = nullptr;
+    unsigned long long* tc_addr = nullptr;
+    int tc_rows = 0;
 };
 
 int generic_rows_per_pass(int rows);

@@ -347,7 +347,9 @@ __global__ __launch_bounds__(256) void k_decode_prepare(int k, int e, int rows_p
                                                         const uint8_t** surv_ptrs,
                                                         uint8_t** out_ptrs, uint4* tabs4,
                                                         uint32_t* ctab, long long tab_block_stride,
-                                                        int* status)
+                                                        int* status,
+                                                        const unsigned long long* tc_table,
+                                                        unsigned long long* tc_addr, int tc_rows)
 {
     extern __shared__ __align__(16) uint8_t lds[];
     uint8_t* gexp = lds;             // 512
@@ -499,6 +501,17 @@ __global__ __launch_bounds__(256) void k_decode_prepare(int k, int e, int rows_p
         out_ptrs[(size_t)b * e + i] = out + ((size_t)b * e + i) * out_pitch;
     if (st != 0)
         return;
+    if (tc_addr && tc_table) {
+        // k_rs_tc handler addresses [j][slot]: coefficient inv(b)[err[slot]][j]
+        // of survivor j (the isa.cpp:184-204 decode rows), padding slots ->
+        // handler 0; the table is [slot parity][coefficient]
+        unsigned long long* ta = tc_addr + (size_t)b * k * tc_rows;
+        for (int idx = tid; idx < k * tc_rows; idx += nt) {
+            const int j = idx / tc_rows, r = idx - j * tc_rows;
+            ta[idx] = tc_table[(r & 1) * 256 + (r < e ? Dm[eb[r] * k + j] : 0)];
+        }
+        return;
+    }
     // tables: [j][rows_pad], rows beyond e zero
     uint4* t4 = tabs4 + (size_t)b * tab_block_stride;
     uint32_t* tc = ctab + (size_t)b * tab_block_stride;
@@ -695,7 +708,7 @@ hipError_t launch_decode_prepare(const PrepArgs& a, hipStream_t st)
     hipLaunchKernelGGL(k_decode_prepare, dim3((unsigned)a.blocks), dim3(256), lds, st, a.k, a.e,
                        a.rows_pad, a.err, a.src, a.src_pitch, a.par, a.par_pitch, a.out,
                        a.out_pitch, a.surv_ptrs, a.out_ptrs, a.tabs4, a.ctab,
-                       a.tab_block_stride, a.status);
+                       a.tab_block_stride, a.status, a.tc_table, a.tc_addr, a.tc_rows);
     return hipGetLastError();
 }
 

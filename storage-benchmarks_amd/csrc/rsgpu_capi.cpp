@@ -833,6 +833,15 @@ static bool use_syn_path(int k, int e, size_t len, size_t pitch, const void* src
            (uintptr_t)src % 16 == 0 && (uintptr_t)par % 16 == 0 && (uintptr_t)out % 16 == 0;
 }
 
+// General decode (k x k inversion) through k_rs_tc: e <= 32 with 32-byte
+// multiple, 16-byte aligned rows (RSGPU_NO_TC=1 keeps k_dot_generic).
+static bool use_tc_general(rsgpu_ctx* ctx, int e, size_t len, size_t pitch, const void* src,
+                           const void* par, const void* out)
+{
+    return len % 32 == 0 && pitch % 16 == 0 && (uintptr_t)src % 16 == 0 && (uintptr_t)par % 16 == 0 &&
+           (uintptr_t)out % 16 == 0 && use_tc(ctx, e);
+}
+
 static void decode_ws_layout(int k, int e, size_t blocks, size_t* off_surv, size_t* off_out,
                              size_t* off_t4, size_t* off_tc, size_t* off_tca, size_t* off_sa,
                              size_t* total)
@@ -919,6 +928,14 @@ int rsgpu_decode_prepare(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch,
     p.ctab = (uint32_t*)(ws + o_tc);
     p.tab_block_stride = (long long)k * rows_pad;
     p.status = d_status;
+    if (use_tc_general(ctx, e, len, pitch, d_src, d_parity, d_out)) {
+        // [blocks][k][tc_rows] spans the tca and sa regions (k >= e)
+        p.tc_table = ctx->d_tc_table;
+        p.tc_addr = (unsigned long long*)(ws + o_tca);
+        p.tc_rows = tc_rows_per_pass(e);
+        p.tabs4 = nullptr;
+        p.ctab = nullptr;
+    }
     KTimer kt(ctx, "k_decode_prepare", blocks);
     RS_HIP(ctx, launch_decode_prepare(p, ctx->stream));
     return RSGPU_OK;
@@ -1030,6 +1047,22 @@ int rsgpu_decode_apply(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch, s
             RS_HIP(ctx, hipEventRecord(ev, solve_stream));
             RS_HIP(ctx, hipStreamWaitEvent(ctx->stream, ev, 0));
         }
+        return RSGPU_OK;
+    }
+    if (use_tc_general(ctx, e, len, pitch, d_src, d_parity, d_out)) {
+        // any geometry, e <= 32, 32-byte-multiple aligned rows: the rows of
+        // inv(b) through the threaded-code kernel (prepared by k_decode_prepare)
+        TcArgs t{};
+        t.srcs = (const uint8_t* const*)(ws + o_surv);
+        t.dsts = (uint8_t* const*)(ws + o_out);
+        t.addr = (const unsigned long long*)(ws + o_tca);
+        t.addr_stride = (long long)k * tc_rows_per_pass(e);
+        t.k = k;
+        t.rows = e;
+        t.len = (long long)len;
+        t.status = d_status;
+        KTimer kt(ctx, "k_rs_tc(decode)", blocks);
+        RS_HIP(ctx, launch_rs_tc(t, (long long)blocks, ctx->stream));
         return RSGPU_OK;
     }
     const bool aligned = ((uintptr_t)d_src % 16 == 0) && ((uintptr_t)d_parity % 16 == 0) &&
