@@ -14,7 +14,7 @@ v0..v63 with amdgpu_num_vgpr(64), so v64..v127 belong to the asm alone):
                         s_set_gpr_idx_on 8*s, gpr_idx(SRC0,DST))
     L[n], H[n], n = 1..15   v[reg_l(n)], v[reg_h(n)] (layouts below)
     return address      s[RET:RET+1]
-    address banks       s[64:79], s[84:99]; m0 save s80; staged planes v[24:31]
+    address banks       s[64:79], s[84:99]; m0 save s63; chain continuation s[80:81]; planes v[24:31]
     (all of these are clobbers of the one asm statement per chunk)
 
 usage: gen_tc_handlers.py OUT.inc [SYN.inc]
@@ -81,7 +81,7 @@ def mat_row(c: int, b: int) -> int:
 # and five SALU per slot pair instead of four and six.
 CHAIN = os.environ.get("RSGPU_TC_CHAIN", "1") == "1"
 NHANDLERS = 512 if CHAIN else 256
-RA = 100
+RA = 80  # s[80:81]; s[100:101] would be a reserved pair on gfx950
 
 
 def handler(c: int, odd: bool = False) -> list:
@@ -119,7 +119,7 @@ def handler_table() -> list:
 PLANE_REG = [reg_l(1), reg_l(2), reg_l(4), reg_l(8), reg_h(1), reg_h(2), reg_h(4), reg_h(8)]
 STAGE = 24       # v[24:31]: next source's planes (staged layout: read one source ahead)
 BANK = (64, 84)  # s[64:79] / s[84:99]: handler addresses of alternate sources
-SM0 = 80         # m0 save
+SM0 = 63         # m0 save
 C = 8            # sources per LDS chunk (rs_tc.hip)
 LDS_T = 2048     # LDS bytes per source: [2 halves][64 lanes] x 16 B
 LDS_H = 1024

@@ -77,6 +77,26 @@ RS_HD inline void gf_build_tables(GfTables& t)
     t.log[0] = 0;
 }
 
+// The same tables as a constant expression (device code copies them into
+// LDS with one load per thread instead of building them serially).
+RS_HD constexpr GfTables make_gf_tables()
+{
+    GfTables t{};
+    unsigned v = 1;
+    for (int i = 0; i < 255; ++i) {
+        t.exp[i] = (uint8_t)v;
+        t.exp[i + 255] = (uint8_t)v;
+        t.log[v] = (uint8_t)i;
+        v <<= 1;
+        if (v & 0x100)
+            v ^= 0x11D;
+    }
+    t.exp[510] = t.exp[0];
+    t.exp[511] = t.exp[1];
+    t.log[0] = 0;
+    return t;
+}
+
 // The v_perm lookup tables of one coefficient c for the runtime-coefficient
 // kernel (see rs_kernels.hip, "generic dot product"):
 //   t[0] = c*{0,1,2,3}        t[1] = c*{4,5,6,7}          (bits 0-2)

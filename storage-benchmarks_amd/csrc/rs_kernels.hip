@@ -339,6 +339,9 @@ __global__ __launch_bounds__(256) void k_rs_encode_lh(const uint8_t* __restrict_
 // c[i][j] = inv(b)[err[i]][j] (isa.cpp:177-204).
 // LDS: two k x k byte matrices + log/antilog tables.
 
+// log / antilog tables of GF(2^8), a compile-time constant (gf256.h)
+__device__ const GfTables kGfTables = make_gf_tables();
+
 __global__ __launch_bounds__(256) void k_decode_prepare(int k, int e, int rows_pad,
                                                         const uint8_t* __restrict__ err,
                                                         const uint8_t* src, long long src_pitch,
@@ -364,19 +367,10 @@ __global__ __launch_bounds__(256) void k_decode_prepare(int k, int e, int rows_p
     const int tid = threadIdx.x, nt = blockDim.x;
     const int m = k + e;
 
-    if (tid == 0) {
-        unsigned v = 1;
-        for (int i = 0; i < 255; ++i) {
-            gexp[i] = (uint8_t)v;
-            gexp[i + 255] = (uint8_t)v;
-            glog[v] = (uint8_t)i;
-            v <<= 1;
-            if (v & 0x100)
-                v ^= 0x11D;
-        }
-        gexp[510] = gexp[0];
-        gexp[511] = gexp[1];
-        glog[0] = 0;
+    for (int i = tid; i < 512; i += nt) {
+        gexp[i] = kGfTables.exp[i];
+        if (i < 256)
+            glog[i] = kGfTables.log[i];
     }
     for (int i = tid; i < 256; i += nt)
         in_err[i] = 0;
@@ -847,19 +841,12 @@ __global__ __launch_bounds__(256) void k_decode_prepare_syn(int k, int e, int ro
     const int b = blockIdx.x;
     const int tid = threadIdx.x, nt = blockDim.x;
     const uint8_t* eb = err + (size_t)b * e;
+    for (int i = tid; i < 512; i += nt) {
+        gexp[i] = kGfTables.exp[i];
+        if (i < 256)
+            glog[i] = kGfTables.log[i];
+    }
     if (tid == 0) {
-        unsigned v = 1;
-        for (int i = 0; i < 255; ++i) {
-            gexp[i] = (uint8_t)v;
-            gexp[i + 255] = (uint8_t)v;
-            glog[v] = (uint8_t)i;
-            v <<= 1;
-            if (v & 0x100)
-                v ^= 0x11D;
-        }
-        gexp[510] = gexp[0];
-        gexp[511] = gexp[1];
-        glog[0] = 0;
         // validate: strictly ascending originals
         int bad = 0;
         unsigned long long m0 = 0, m1 = 0;
@@ -882,15 +869,101 @@ __global__ __launch_bounds__(256) void k_decode_prepare_syn(int k, int e, int ro
             status[b] = sh[0];
         return;
     }
+    auto gmul = [&](uint8_t x, uint8_t y) -> uint8_t {
+        return (x && y) ? gexp[glog[x] + glog[y]] : (uint8_t)0;
+    };
+    if (dir_addr && tc_table) {
+        // One-matrix decode through k_rs_tc: sources = the k - e surviving
+        // originals (ascending) then the e parity rows, outputs = the erased
+        // originals.  d_E = V_E^-1 (P ^ V_kept d_kept), V_E[p][i] = a_i^p with
+        // a_i = 2^(j_i) (gf_gen_rs_matrix rows k + p, isa/ec_base.c:71-78):
+        // the rows of inv(b) that isa.cpp:177-209 applies (the unique
+        // solution, so bit-exact with the reference's decode).  V_E is
+        // Vandermonde in distinct points, so it is never singular, and both
+        // blocks have closed forms (Lagrange basis L_i of the points a_l,
+        // Lambda(z) = prod_l (z + a_l), w_i = prod_{l != i} (a_i + a_l)):
+        //   (V_E^-1)[i][p]          = [z^p] L_i(z) = [z^p] (Lambda(z) / (z + a_i)) / w_i
+        //   (V_E^-1 V_kept)[i][q]   = L_i(b_q)     = Lambda(b_q) / ((b_q + a_i) w_i)
+        // with b_q = 2^(j_q) for survivor q: O(e k) work, no elimination.
+        uint8_t* lv = Dm + e * e;  // survivors, k - e bytes (256 reserved)
+        uint8_t* lam = lv + 256;   // Lambda coefficients, e + 1 (64 reserved)
+        uint8_t* lw = lam + 64;    // log w_i (64 reserved)
+        uint8_t* lb = lw + 64;     // log Lambda(b_q) (256 reserved)
+        const int nl = k - e;
+        for (int j = tid; j < k; j += nt) {
+            int below = 0;  // erased originals < j (the list is validated ascending)
+            bool er = false;
+            for (int i = 0; i < e; ++i) {
+                below += eb[i] < j;
+                er |= eb[i] == j;
+            }
+            if (!er)
+                lv[j - below] = (uint8_t)j;
+        }
+        if (tid < 64) {  // Lambda(z) by wave 0, lane m holding the coefficient of z^m
+            uint8_t lm = tid == 0 ? 1 : 0;  // e <= 32 < 64 lanes
+            for (int l = 0; l < e; ++l) {   // times (z + a_l): lam_m <- lam_{m-1} + a_l lam_m
+                const int below = __shfl_up((int)lm, 1);
+                lm = (uint8_t)(tid == 0 ? 0 : below) ^ gmul(gexp[eb[l]], lm);
+            }
+            if (tid <= e)
+                lam[tid] = lm;
+        }
+        for (int i = tid; i < e; i += nt) {
+            const uint8_t a = gexp[eb[i]];
+            int lg = 0;
+            for (int l = 0; l < e; ++l)
+                if (l != i)
+                    lg += glog[a ^ gexp[eb[l]]];
+            lw[i] = (uint8_t)(lg % 255);
+        }
+        __syncthreads();
+        for (int q = tid; q < nl; q += nt) {  // log Lambda(b_q) = sum_l log(b_q + a_l), never 0
+            const uint8_t bq = gexp[lv[q]];
+            int lg = 0;
+            for (int l = 0; l < e; ++l)
+                lg += glog[bq ^ gexp[eb[l]]];
+            lb[q] = (uint8_t)(lg % 255);
+        }
+        for (int i = tid; i < e; i += nt) {  // row i of V_E^-1 by synthetic division
+            const uint8_t a = gexp[eb[i]];
+            uint8_t qm = lam[e];  // q_{e-1}
+            for (int m = e - 1; m >= 0; --m) {
+                A[i * e + m] = qm ? gexp[(glog[qm] + 255 - lw[i]) % 255] : (uint8_t)0;
+                if (m)
+                    qm = lam[m] ^ gmul(a, qm);
+            }
+        }
+        __syncthreads();
+        if (tid == 0)
+            status[b] = 0;
+        for (int q = tid; q < k; q += nt)
+            srcs[(size_t)b * k + q] = q < nl ? src + ((size_t)b * k + lv[q]) * out_pitch
+                                             : par + ((size_t)b * e + (q - nl)) * out_pitch;
+        for (int i = tid; i < e; i += nt)
+            dsts[(size_t)b * e + i] = out + ((size_t)b * e + i) * out_pitch;
+        unsigned long long* da = dir_addr + (size_t)b * k * tc_rows;
+        for (int idx = tid; idx < k * tc_rows; idx += nt) {
+            const int q = idx / tc_rows, i = idx - q * tc_rows;
+            uint8_t c = 0;
+            if (i < e) {
+                if (q < nl) {
+                    const uint8_t d = gexp[lv[q]] ^ gexp[eb[i]];  // b_q + a_i, never 0
+                    c = gexp[(lb[q] + 2 * 255 - glog[d] - lw[i]) % 255];
+                } else {
+                    c = A[i * e + (q - nl)];
+                }
+            }
+            da[idx] = tc_table[(i & 1) * 256 + c];
+        }
+        return;
+    }
     for (int idx = tid; idx < e * e; idx += nt) {
         const int p = idx / e, i = idx - p * e;
         A[idx] = gexp[(p * (int)eb[i]) % 255];
         Dm[idx] = (p == i) ? 1 : 0;
     }
     __syncthreads();
-    auto gmul = [&](uint8_t x, uint8_t y) -> uint8_t {
-        return (x && y) ? gexp[glog[x] + glog[y]] : (uint8_t)0;
-    };
     const int n = e;
     for (int i = 0; i < n; ++i) {
         if (tid == 0) {
@@ -961,50 +1034,6 @@ __global__ __launch_bounds__(256) void k_decode_prepare_syn(int k, int e, int ro
     }
     if (st != 0)
         return;
-    if (dir_addr && tc_table) {
-        // One-matrix decode through k_rs_tc: sources = the k - e surviving
-        // originals (ascending) then the e parity rows, outputs = the erased
-        // originals.  d_E = V_E^-1 (P ^ V_kept d_kept), so the coefficient of
-        // survivor q (original lv[q]) for output i is
-        //   sum_p (V_E^-1)[i][p] 2^(p lv[q])   (gf_gen_rs_matrix rows k + p,
-        // isa/ec_base.c:71-78), and of parity row p it is (V_E^-1)[i][p]:
-        // the rows of inv(b) that isa.cpp:177-209 applies (the unique
-        // solution, so bit-exact with the reference's decode).
-        uint8_t* lv = Dm + e * e;  // live list, k - e bytes
-        for (int j = tid; j < k; j += nt) {
-            int below = 0;  // erased originals < j (the list is validated ascending)
-            bool er = false;
-            for (int i = 0; i < e; ++i) {
-                below += eb[i] < j;
-                er |= eb[i] == j;
-            }
-            if (!er)
-                lv[j - below] = (uint8_t)j;
-        }
-        __syncthreads();
-        const int nl = k - e;
-        for (int q = tid; q < k; q += nt)
-            srcs[(size_t)b * k + q] = q < nl ? src + ((size_t)b * k + lv[q]) * out_pitch
-                                             : par + ((size_t)b * e + (q - nl)) * out_pitch;
-        for (int i = tid; i < e; i += nt)
-            dsts[(size_t)b * e + i] = out + ((size_t)b * e + i) * out_pitch;
-        unsigned long long* da = dir_addr + (size_t)b * k * tc_rows;
-        for (int idx = tid; idx < k * tc_rows; idx += nt) {
-            const int q = idx / tc_rows, i = idx - q * tc_rows;
-            uint8_t c = 0;
-            if (i < e) {
-                if (q < nl) {
-                    const int j = lv[q];
-                    for (int p = 0; p < e; ++p)
-                        c ^= gmul(Dm[i * n + p], gexp[(p * j) % 255]);
-                } else {
-                    c = Dm[i * n + (q - nl)];
-                }
-            }
-            da[idx] = tc_table[(i & 1) * 256 + c];
-        }
-        return;
-    }
     if (syn_addr && tc_table) {
         // syndrome phase of the fused decode (threaded code): the q-th
         // surviving original j_q (ascending) carries coefficient 2^(r j_q)
@@ -1066,7 +1095,7 @@ __global__ __launch_bounds__(256) void k_decode_prepare_syn(int k, int e, int ro
     }
 }
 
-size_t decode_prepare_syn_lds_bytes(int e) { return 832 + 2 * (size_t)e * e + 256; }
+size_t decode_prepare_syn_lds_bytes(int e) { return 832 + 2 * (size_t)e * e + 256 + 384; }
 
 hipError_t launch_decode_prepare_syn(int k, int e, int rows_pad, long long blocks,
                                      const uint8_t* err, uint8_t* out, long long out_pitch,
