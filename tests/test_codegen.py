@@ -213,3 +213,34 @@ def test_chunk_dispatch(nt):
             exp = [x ^ g.gf_mul(coef[t][s], y) for x, y in zip(exp, src[t])]
         assert unplanes([regs[g.ACC + 8 * s + a] for a in range(8)]) == exp, (nt, s)
 
+
+
+import gen_enc_progs as ge  # noqa: E402
+
+
+def test_encode_programs_cover_every_output():
+    """Every generated per-source XOR program of k_rs_bs (gen_enc_progs.py):
+    each composite is an XOR of earlier values, and every output plane of
+    every row equals the plane mask of 2^(r T) (gf_gen_rs_matrix
+    coefficient) -- evaluated symbolically over the 8 source planes."""
+    nblk = 0
+    for K, E, C, NW in ge.PLANS:
+        opw = (E + NW - 1) // NW
+        for grp in range(NW):
+            R0, NR = grp * opw, min(opw, E - grp * opw)
+            for T in range(C):
+                ops, vals, outs = ge.block(K, E, C, R0, NR, T)
+                V = [1 << a for a in range(8)]
+                for op in ops:
+                    assert all(i < len(V) or i == ge.NONE for i in op)
+                    x = 0
+                    for i in op:
+                        if i != ge.NONE:
+                            x ^= V[i]
+                    V.append(x)
+                for o, (x, y) in enumerate(outs):
+                    r, b = R0 + o // 8, o % 8
+                    got = (V[x] if x != ge.NONE else 0) ^ (V[y] if y != ge.NONE else 0)
+                    assert got == ge.mat_row(ge.gf_pow2(r * T), b), (K, E, C, R0, T, o)
+                nblk += 1
+    assert nblk == 233
