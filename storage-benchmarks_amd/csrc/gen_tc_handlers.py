@@ -365,8 +365,8 @@ def main() -> None:
     # the accumulators live only in asm-owned v[ACC:ACC+63] (the kernel caps
     # the compiler at v0..v{ACC-1}): zeroed, consumed and read out by asm
     lines.append("#define RSGPU_TC_ZERO \\")
-    for i in range(64):
-        lines.append(f'    "v_mov_b32 v{ACC + i}, 0\\n" \\')
+    for i in range(0, 64, 2):  # v_mov_b64: two accumulator planes per instruction
+        lines.append(f'    "v_mov_b64 v[{ACC + i}:{ACC + i + 1}], 0\\n" \\')
     lines.append("")
     for slot in range(8):
         body = "".join(f"v_mov_b32 %{q}, v{ACC + 8 * slot + q}\\n" for q in range(8))
