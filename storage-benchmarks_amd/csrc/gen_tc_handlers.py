@@ -33,24 +33,36 @@ STRIDE = 72  # 8 x 8-byte VOP3 + s_setpc_b64 (4) + s_nop pad (4)
 # staging copies); the 11 composite L entries follow at v32.., then the 11 H.
 # "staged" layout (RSGPU_TC_LAYOUT=staged): L[n] = v[31 + n], H[n] = v[46 + n],
 # planes read one source ahead into v24..v31 and copied in (8 v_mov).
+# "dbuf" (RSGPU_TC_LAYOUT=dbuf, experiment): two plane sets, v24..v31 and
+# v54..v61, used by alternate sources, so the next source's planes are read
+# one source ahead without copies; a second handler copy reads set B (the
+# copy is chosen by SOURCE parity, so the slot-pair chain is off).
 LAYOUT = os.environ.get("RSGPU_TC_LAYOUT", "late")
-assert LAYOUT in ("late", "staged"), LAYOUT
+assert LAYOUT in ("late", "staged", "dbuf"), LAYOUT
+PB = 54  # plane set B of the dbuf layout
 _COMPOSITE = [n for n in range(1, 16) if n & (n - 1)]
 
 
-def reg_l(n: int) -> int:
+def reg_l(n: int, pset: int = 0) -> int:
     if LAYOUT == "staged":
         return 31 + n
-    return 24 + (n.bit_length() - 1) if n & (n - 1) == 0 else 32 + _COMPOSITE.index(n)
+    single = n & (n - 1) == 0
+    if single and pset:
+        return PB + (n.bit_length() - 1)
+    return 24 + (n.bit_length() - 1) if single else 32 + _COMPOSITE.index(n)
 
 
-def reg_h(n: int) -> int:
+def reg_h(n: int, pset: int = 0) -> int:
     if LAYOUT == "staged":
         return 46 + n
-    return 28 + (n.bit_length() - 1) if n & (n - 1) == 0 else 43 + _COMPOSITE.index(n)
+    single = n & (n - 1) == 0
+    if single and pset:
+        return PB + 4 + (n.bit_length() - 1)
+    return 28 + (n.bit_length() - 1) if single else 43 + _COMPOSITE.index(n)
 
 
-TABLE_REGS = sorted({reg_l(n) for n in range(1, 16)} | {reg_h(n) for n in range(1, 16)})
+TABLE_REGS = sorted({reg_l(n) for n in range(1, 16)} | {reg_h(n) for n in range(1, 16)} |
+                    (set(range(PB, PB + 8)) if LAYOUT == "dbuf" else set()))
 
 
 def gf_mul(a: int, b: int) -> int:
@@ -79,8 +91,8 @@ def mat_row(c: int, b: int) -> int:
 # the odd handler whose address the chunk put in s[RA:RA+1]; the odd handler
 # works on slot 2p+1 (v[ACC+8..], same relocation) and returns.  Three jumps
 # and five SALU per slot pair instead of four and six.
-CHAIN = os.environ.get("RSGPU_TC_CHAIN", "1") == "1"
-NHANDLERS = 512 if CHAIN else 256
+CHAIN = os.environ.get("RSGPU_TC_CHAIN", "1") == "1" and LAYOUT != "dbuf"
+NHANDLERS = 512 if CHAIN or LAYOUT == "dbuf" else 256
 RA = 80  # s[80:81]; s[100:101] would be a reserved pair on gfx950
 
 
@@ -88,6 +100,7 @@ def handler(c: int, odd: bool = False) -> list:
     """Handler of coefficient c; `odd` = the odd-slot copy of chained mode."""
     ret = RA if CHAIN and not odd else RET
     base = ACC + 8 if CHAIN and odd else ACC
+    ps = 1 if LAYOUT == "dbuf" and odd else 0
     if c == 0:
         # no-op: continue at once; pad to STRIDE with never-executed s_nop
         return [f"s_setpc_b64 s[{ret}:{ret + 1}]"] + ["s_nop 0"] * ((STRIDE - 4) // 4)
@@ -97,11 +110,11 @@ def handler(c: int, odd: bool = False) -> list:
         lo, hi = m & 15, m >> 4
         acc = base + b
         if lo and hi:
-            ins.append(f"v_bitop3_b32 v{acc}, v{acc}, v{reg_l(lo)}, v{reg_h(hi)} bitop3:0x96")
+            ins.append(f"v_bitop3_b32 v{acc}, v{acc}, v{reg_l(lo, ps)}, v{reg_h(hi, ps)} bitop3:0x96")
         elif lo:
-            ins.append(f"v_xor_b32_e64 v{acc}, v{acc}, v{reg_l(lo)}")
+            ins.append(f"v_xor_b32_e64 v{acc}, v{acc}, v{reg_l(lo, ps)}")
         elif hi:
-            ins.append(f"v_xor_b32_e64 v{acc}, v{acc}, v{reg_h(hi)}")
+            ins.append(f"v_xor_b32_e64 v{acc}, v{acc}, v{reg_h(hi, ps)}")
         else:  # a nonzero c has an invertible matrix: no zero rows
             raise AssertionError("zero row for nonzero coefficient")
     ins.append(f"s_setpc_b64 s[{ret}:{ret + 1}]")
@@ -112,7 +125,7 @@ def handler(c: int, odd: bool = False) -> list:
 def handler_table() -> list:
     """All handlers in address order: c = 0..255 (even / only copy), then in
     chained mode the odd copy.  Handler number h lives at base + h * STRIDE."""
-    return [i for odd in ((False, True) if CHAIN else (False,)) for c in range(256)
+    return [i for odd in ((False, True) if NHANDLERS == 512 else (False,)) for c in range(256)
             for i in handler(c, odd)]
 
 
@@ -134,13 +147,30 @@ def chunk(nt: int) -> list:
     Operands: %[la] = LDS byte address of the chunk + lane*16, %[pa] = address
     table of source 0 (this wave's 8 slots), %[o1].. = byte offsets of
     sources 1.. in that table."""
-    def stage(t):
-        return [f"ds_read_b128 v[{STAGE}:{STAGE + 3}], %[la] offset:{t * LDS_T}",
-                f"ds_read_b128 v[{STAGE + 4}:{STAGE + 7}], %[la] offset:{t * LDS_T + LDS_H}"]
+    def stage(t, dst=STAGE):
+        return [f"ds_read_b128 v[{dst}:{dst + 3}], %[la] offset:{t * LDS_T}",
+                f"ds_read_b128 v[{dst + 4}:{dst + 7}], %[la] offset:{t * LDS_T + LDS_H}"]
 
     def sload(t, bank):
         off = "0" if t == 0 else f"%[o{t}]"
         return [f"s_load_dwordx16 s[{bank}:{bank + 15}], %[pa], {off}"]
+
+    if LAYOUT == "dbuf":
+        ins = [f"s_mov_b32 s{SM0}, m0"] + sload(0, BANK[0]) + stage(0, STAGE)
+        for t in range(nt):
+            cur, nxt = BANK[t & 1], BANK[(t + 1) & 1]
+            ins.append("s_waitcnt lgkmcnt(0)")
+            if t + 1 < nt:  # the other plane set is idle: read one source ahead
+                ins += sload(t + 1, nxt) + stage(t + 1, PB if t % 2 == 0 else STAGE)
+            ins += tables(t & 1)
+            ins.append("s_set_gpr_idx_on 0, gpr_idx(SRC0,DST)")
+            for slot in range(8):
+                if slot:
+                    ins.append(f"s_set_gpr_idx_idx {8 * slot}")
+                ins.append(f"s_swappc_b64 s[{RET}:{RET + 1}], s[{cur + 2 * slot}:{cur + 2 * slot + 1}]")
+            ins.append("s_set_gpr_idx_off")
+        ins += [f"s_mov_b32 m0, s{SM0}", "s_nop 0"]
+        return ins
 
     late = LAYOUT == "late"
     ins = [f"s_mov_b32 s{SM0}, m0"] + sload(0, BANK[0]) + stage(0)
@@ -211,13 +241,14 @@ def mac_lines(c: int, slot: int) -> list:
     return ins
 
 
-def tables() -> list:
+def tables(pset: int = 0) -> list:
+    """The 22 composite entries from plane set `pset` (dbuf layout: 1 = B)."""
     ins = []
     for reg in (reg_l, reg_h):
         for n in range(1, 16):
             low = n & -n
             if n != low:
-                ins.append(f"v_xor_b32_e32 v{reg(n)}, v{reg(n ^ low)}, v{reg(low)}")
+                ins.append(f"v_xor_b32_e32 v{reg(n)}, v{reg(n ^ low, pset)}, v{reg(low, pset)}")
     return ins
 
 
@@ -350,6 +381,7 @@ def main() -> None:
         f"#define RSGPU_TC_ACC {ACC}",
         f"#define RSGPU_TC_LAYOUT_{LAYOUT.upper()} 1",
         f"#define RSGPU_TC_NHANDLERS {NHANDLERS}",
+        f"#define RSGPU_TC_COPY_BY_SOURCE {1 if LAYOUT == 'dbuf' else 0}",
         f"#define RSGPU_TC_RET {RET}",
         "#define RSGPU_TC_HANDLERS \\",
     ]

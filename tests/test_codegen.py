@@ -45,13 +45,14 @@ def unplanes(p):
     return [sum(((p[a] >> i) & 1) << a for a in range(8)) for i in range(32)]
 
 
-def load_tables(regs, by):
-    """The four-Russians tables of one source: single-bit entries = planes,
-    the rest built by the generator's own table code."""
+def load_tables(regs, by, pset=0):
+    """The four-Russians tables of one source: single-bit entries = planes
+    (plane set `pset` of the dbuf layout), the rest built by the generator's
+    own table code."""
     p = planes(by)
-    for a, r in enumerate(g.PLANE_REG):
-        regs[r] = p[a]
-    run(g.tables(), regs)
+    for a in range(8):
+        regs[(g.reg_l if a < 4 else g.reg_h)(1 << (a % 4), pset)] = p[a]
+    run(g.tables(pset), regs)
 
 
 @pytest.mark.parametrize("c", range(256))
@@ -61,7 +62,7 @@ def test_handler_multiplies(c):
         regs = {i: 0 for i in range(256)}
         src = [rng.randrange(256) for _ in range(32)]
         acc = [rng.randrange(256) for _ in range(32)]
-        load_tables(regs, src)
+        load_tables(regs, src, 1 if g.LAYOUT == "dbuf" and odd else 0)
         base = g.ACC + (8 if g.CHAIN and odd else 0)
         for a, v in enumerate(planes(acc)):
             regs[base + a] = v
@@ -184,7 +185,10 @@ def test_chunk_dispatch(nt):
             sregs[int(m.group(1))] = sregs[int(m.group(2))]
         elif i.startswith("s_swappc"):
             assert idx is not None
-            c, odd = sregs[int(SWAP.match(i).group(1))], False
+            reg = int(SWAP.match(i).group(1))
+            # dbuf layout: the handler copy follows the source parity, i.e.
+            # which address bank the chunk dispatches from
+            c, odd = sregs[reg], g.LAYOUT == "dbuf" and g.BANK[1] <= reg < g.BANK[1] + 16
             while True:  # a handler, and in chained mode the one it jumps to
                 body = g.handler(c, odd)
                 for h in body:
@@ -202,6 +206,7 @@ def test_chunk_dispatch(nt):
                 tgt = int(SETPC.search(" ".join(body)).group(1))
                 if tgt == g.RET:
                     break
+                assert g.LAYOUT != "dbuf"
                 assert g.CHAIN and tgt == g.RA and not odd
                 c, odd = sregs[g.RA], True
         elif not i.startswith("s_"):

@@ -72,9 +72,15 @@ int main(int argc, char** argv)
     }
     auto table = [&](size_t n) {
         std::vector<unsigned long long> v(n);
-        for (size_t i = 0; i < n; ++i)  // odd slots: the odd-slot copy when chained
-            v[i] = q[0] + (unsigned long long)((tc_handler_count() == 512 && (i & 1) ? 256 : 0) +
+        for (size_t i = 0; i < n; ++i) {  // the handler copy of slot / source parity
+#if RSGPU_TC_COPY_BY_SOURCE
+            const bool odd = (i / 32 % k) & 1;  // dbuf layout: copy by source parity
+#else
+            const bool odd = i & 1;             // chained slot pairs: copy by slot parity
+#endif
+            v[i] = q[0] + (unsigned long long)((tc_handler_count() == 512 && odd ? 256 : 0) +
                                                1 + rng() % nc) * tc_handler_stride();
+        }
         unsigned long long* d;
         (void)hipMalloc(&d, n * 8);
         (void)hipMemcpy(d, v.data(), n * 8, hipMemcpyHostToDevice);
