@@ -799,6 +799,7 @@ static bool use_tc(rsgpu_ctx* ctx, int e)
 //                     parity rows with the e x k decode rows (one pass, HBM
 //                     traffic (k + e) L per block)
 //   fused             k_rs_decode_fused: syndromes + e x e solve per tile
+//                     (the default for k 100, e 20, where it measured faster)
 //                     (instantiated codes only)
 //   split             k_rs_bs syndromes to HBM, then the in-place k_rs_tc solve
 // RSGPU_NO_FUSED=1 (older switch) means split.
@@ -806,15 +807,23 @@ enum class DecodeMode { direct, fused, split };
 
 static DecodeMode decode_mode(int k, int e)
 {
-    static const DecodeMode m = [] {
+    // -1: no override, per-code default below
+    static const int forced = [] {
         const char* v = std::getenv("RSGPU_DECODE");
         const char* nf = std::getenv("RSGPU_NO_FUSED");
         if (v && std::strcmp(v, "fused") == 0)
-            return DecodeMode::fused;
+            return (int)DecodeMode::fused;
         if ((v && std::strcmp(v, "split") == 0) || (nf && nf[0] == '1'))
-            return DecodeMode::split;
-        return DecodeMode::direct;
+            return (int)DecodeMode::split;
+        if (v && std::strcmp(v, "direct") == 0)
+            return (int)DecodeMode::direct;
+        return -1;
     }();
+    DecodeMode m = DecodeMode::direct;
+    if (forced >= 0)
+        m = (DecodeMode)forced;
+    else if (k == 100 && e == 20)
+        m = DecodeMode::fused;  // measured 2 % faster there (BASELINE C5)
     if (m == DecodeMode::fused && !rs_decode_fused_available(k, e))
         return DecodeMode::split;
     return m;

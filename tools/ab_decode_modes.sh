@@ -1,5 +1,7 @@
-# Decode kernel choice A/B per BASELINE config, same box:  bash tools/ab_decode_modes.sh
+# Decode kernel choice A/B per BASELINE config, same box:
+#   bash tools/ab_decode_modes.sh [configs...]   (default: c5 c3 c2)
 set -o pipefail
 O=gpurun_out/modes; mkdir -p $O
 T="timeout -k 10 300"
-for c in c5 c3 c2; do for m in direct fused; do RSGPU_DECODE=$m $T python3 bench.py --config $c --steps 5 --warmup 2 --no-cpu-baseline > $O/${c}_$m.log 2>&1 || exit 1; done; done
+CFGS=${@:-c5 c3 c2}
+for c in $CFGS; do for m in direct fused; do RSGPU_DECODE=$m $T python3 bench.py --config $c --steps 5 --warmup 2 --no-cpu-baseline > $O/${c}_$m.log 2>&1 || exit 1; done; done
