@@ -1,32 +1,39 @@
 // rs_tc.hip -- bit-sliced GF(2^8) dot product with RUNTIME coefficients via
-// threaded code: out_i = sum_p c[i][p] * src_p for per-block matrices c
-// (the decode solve x = V_E^-1 s of the syndrome decoder, rsgpu_capi.cpp).
+// threaded code: out_i = sum_p c[i][p] * src_p for per-block matrices c.
+// Uses: the decode (the e x k rows of inv(b) over the k - e survivors and the
+// e parity rows, rsgpu_capi.cpp / k_decode_prepare_syn; or the rows of the
+// k x k inversion for codes without compile-time kernels), the split
+// decode's solve, and every runtime-coefficient encode (ec_encode_data with
+// any tables, Cauchy).
 //
 // The bit-sliced multiply-accumulate of one coefficient is 8 full-rate
 // v_bitop3 whose REGISTER operands depend on the coefficient value
 // (rs_bitsliced.hip, gen_tc_handlers.py).  Register numbers cannot be chosen
 // at run time without indexing overhead, so all 256 variants exist as code:
-// handler c (72 bytes, generated) applies coefficient c to accumulator slot 0
-// from the four-Russians tables of the current source, and returns with
-// s_setpc_b64.  The kernel dispatches one coefficient with
-//     s_set_gpr_idx_on 8*slot, gpr_idx(SRC0,DST)   (accumulator slot)
-//     s_swappc_b64 ret, addr[slot]                 (handler of the coefficient)
-// where the 8 handler addresses of a source are one s_load_dwordx16 of a
-// table the prepare kernel writes (address = base + c * 72).  Measured on
-// gfx950: ~25-35 SIMD cycles per coefficient and 32 bytes, against ~120 for
-// the v_perm table lookups of k_dot_generic (profiles/r1_ubench_jump.log).
+// handler c (RSGPU_TC_STRIDE = 72 bytes, generated) applies coefficient c to
+// an accumulator slot from the four-Russians tables of the current source.
+// Slot s is reached by GPR indexing (s_set_gpr_idx_on / _idx, one index per
+// slot pair), and the handlers chain in slot pairs: the kernel s_swappc's to
+// the even slot's handler, which jumps to the odd slot's handler (a second
+// copy of the 256 working on the next 8 accumulators), which returns.  The 8
+// handler addresses of a source are one s_load_dwordx16 of the table the
+// prepare kernel writes ([source][slot], address of handler copy (slot & 1)
+// for coefficient c).  GPR index mode costs every VALU it covers about one
+// issue cycle (tools/ubench_idx.hip), the price of reusing one table build
+// for 8 rows without per-slot handler copies.
 //
 // Register contract (gen_tc_handlers.py): accumulators v[64:127] (8 slots x 8
-// planes), L/H tables v[32:61] with the source planes pinned at their
-// single-bit entries, the next source's planes staged in v[24:31] and its
-// handler addresses in the other of two banks s[64:79] / s[84:99] while the
-// current source dispatches (one asm statement per LDS chunk, so every load
-// it starts is also waited for inside it), return address s[82:83].
-// The kernel therefore uses exactly 128 VGPRs: 4 waves per SIMD.
+// planes); the source planes v[24:31] (read from LDS straight into the
+// single-plane table entries after the previous source's dispatch) and the
+// 22 composite L/H entries v[32:53]; handler addresses in the other of two
+// banks s[64:79] / s[84:99] while the current source dispatches (one asm
+// statement per LDS part, so every load it starts is also waited for inside
+// it); return address s[82:83], chain continuation s[80:81], M0 saved in s63.
+// The kernel uses exactly 128 VGPRs: 4 waves per SIMD.
 //
 // Work split: as k_rs_bs -- a workgroup of NW waves covers 64 lanes x 32 bytes
 // of every row of one block; wave w owns output rows [8w, 8w+8); the waves
-// share the loading + bit transposing of each chunk of C sources through LDS.
+// share the loading + bit transposing of each part of C sources through LDS.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
