@@ -260,6 +260,7 @@ def main():
     dom_ms = tot / n
     dom_bytes = alg.get(dom, 0.0) * nb / n      # algorithmic bytes per launch
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
+    read_bytes = float(k * L) * nb / n if alg.get(dom, 0.0) else 0.0
     # PMC bytes per launch come from a separate rocprofv3 --pmc pass of the
     # same command (counters cannot be read inside this timed run); only
     # valid for the C3 workload they were measured on
@@ -285,7 +286,10 @@ def main():
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic, "traffic_source": traffic_src,
-                     "alg_bytes_per_launch": dom_bytes, "avg_ms": round(dom_ms, 3)},
+                     "alg_bytes_per_launch": dom_bytes, "avg_ms": round(dom_ms, 3),
+                     # north_star's HBM-read variant: only the k source rows read
+                     # per block count
+                     "frac_read": round(read_bytes / (dom_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)},
         "cpu_baseline": None,
     }
     if args.host_io and rank == 0:
