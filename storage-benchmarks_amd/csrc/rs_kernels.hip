@@ -889,13 +889,20 @@ __global__ __launch_bounds__(256) void k_decode_prepare_syn(int k, int e, int ro
         uint8_t* lam = lv + 256;   // Lambda coefficients, e + 1 (64 reserved)
         uint8_t* lw = lam + 64;    // log w_i (64 reserved)
         uint8_t* lb = lw + 64;     // log Lambda(b_q) (256 reserved)
+        uint8_t* ea = lb + 256;    // the erased originals j_i (64 reserved)
+        uint8_t* aa = ea + 64;     // a_i = 2^(j_i) (64 reserved)
         const int nl = k - e;
+        for (int i = tid; i < e; i += nt) {  // the list once from global memory
+            ea[i] = eb[i];
+            aa[i] = gexp[eb[i]];
+        }
+        __syncthreads();
         for (int j = tid; j < k; j += nt) {
             int below = 0;  // erased originals < j (the list is validated ascending)
             bool er = false;
             for (int i = 0; i < e; ++i) {
-                below += eb[i] < j;
-                er |= eb[i] == j;
+                below += ea[i] < j;
+                er |= ea[i] == j;
             }
             if (!er)
                 lv[j - below] = (uint8_t)j;
@@ -904,17 +911,17 @@ __global__ __launch_bounds__(256) void k_decode_prepare_syn(int k, int e, int ro
             uint8_t lm = tid == 0 ? 1 : 0;  // e <= 32 < 64 lanes
             for (int l = 0; l < e; ++l) {   // times (z + a_l): lam_m <- lam_{m-1} + a_l lam_m
                 const int below = __shfl_up((int)lm, 1);
-                lm = (uint8_t)(tid == 0 ? 0 : below) ^ gmul(gexp[eb[l]], lm);
+                lm = (uint8_t)(tid == 0 ? 0 : below) ^ gmul(aa[l], lm);
             }
             if (tid <= e)
                 lam[tid] = lm;
         }
         for (int i = tid; i < e; i += nt) {
-            const uint8_t a = gexp[eb[i]];
+            const uint8_t a = aa[i];
             int lg = 0;
             for (int l = 0; l < e; ++l)
                 if (l != i)
-                    lg += glog[a ^ gexp[eb[l]]];
+                    lg += glog[a ^ aa[l]];
             lw[i] = (uint8_t)(lg % 255);
         }
         __syncthreads();
@@ -922,11 +929,11 @@ __global__ __launch_bounds__(256) void k_decode_prepare_syn(int k, int e, int ro
             const uint8_t bq = gexp[lv[q]];
             int lg = 0;
             for (int l = 0; l < e; ++l)
-                lg += glog[bq ^ gexp[eb[l]]];
+                lg += glog[bq ^ aa[l]];
             lb[q] = (uint8_t)(lg % 255);
         }
         for (int i = tid; i < e; i += nt) {  // row i of V_E^-1 by synthetic division
-            const uint8_t a = gexp[eb[i]];
+            const uint8_t a = aa[i];
             uint8_t qm = lam[e];  // q_{e-1}
             for (int m = e - 1; m >= 0; --m) {
                 A[i * e + m] = qm ? gexp[(glog[qm] + 255 - lw[i]) % 255] : (uint8_t)0;
@@ -948,7 +955,7 @@ __global__ __launch_bounds__(256) void k_decode_prepare_syn(int k, int e, int ro
             uint8_t c = 0;
             if (i < e) {
                 if (q < nl) {
-                    const uint8_t d = gexp[lv[q]] ^ gexp[eb[i]];  // b_q + a_i, never 0
+                    const uint8_t d = gexp[lv[q]] ^ aa[i];  // b_q + a_i, never 0
                     c = gexp[(lb[q] + 2 * 255 - glog[d] - lw[i]) % 255];
                 } else {
                     c = A[i * e + (q - nl)];
@@ -1095,7 +1102,7 @@ __global__ __launch_bounds__(256) void k_decode_prepare_syn(int k, int e, int ro
     }
 }
 
-size_t decode_prepare_syn_lds_bytes(int e) { return 832 + 2 * (size_t)e * e + 256 + 384; }
+size_t decode_prepare_syn_lds_bytes(int e) { return 832 + 2 * (size_t)e * e + 256 + 512; }
 
 hipError_t launch_decode_prepare_syn(int k, int e, int rows_pad, long long blocks,
                                      const uint8_t* err, uint8_t* out, long long out_pitch,
