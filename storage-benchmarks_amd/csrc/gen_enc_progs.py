@@ -13,6 +13,10 @@ values (planes or composites), each composite costing one 2- or 3-input XOR
 of values already available.  On the (64, 32) plan that is 12.1 composites
 per source instead of 22; the accumulation stays one instruction per output.
 
+Also the Horner twiddles (row r times 2^(C r) between chunks) as XOR
+programs over the row's 8 accumulator planes: TwProg<K, E, C, R> with NOPS,
+ops (as below) and outs[8] = the value that becomes plane b.
+
 Output: C++ specializations EncProg<K, E, C, R0, NR, T> with
   NOPS, ops[NOPS][3]  value 8 + i = XOR of values ops[i][0..2] (255 = none)
   outs[NR * 8][2]     acc[s][b] ^= values outs[s*8+b][0] ^ outs[s*8+b][1]
@@ -107,6 +111,53 @@ def program(masks):
     return ops, vals, pair
 
 
+def twiddle(c):
+    """XOR program of the in-register map x -> c x on 8 planes (a Horner
+    twiddle): outputs are masks over the input planes; greedy: whenever an
+    output is one 2- or 3-input XOR of available values, build it, else add
+    the 3-input XOR that makes the most outputs reachable."""
+    outs_m = [mat_row(c, b) for b in range(8)]
+    vals = [1 << a for a in range(8)]
+    have = {m: i for i, m in enumerate(vals)}
+    ops = []
+
+    def one_op(m):
+        for a, b in itertools.combinations(list(have), 2):
+            if a ^ b == m:
+                return (have[a], have[b], NONE)
+        for a, b, d in itertools.combinations(list(have), 3):
+            if a ^ b ^ d == m:
+                return (have[a], have[b], have[d])
+        return None
+
+    need = [m for m in dict.fromkeys(outs_m) if m not in have]
+    while need:
+        done = None
+        for m in need:
+            src = one_op(m)
+            if src:
+                done = (m, src)
+                break
+        if done is None:
+            best, best_n, best_src = None, -1, None
+            for a, b, d in itertools.combinations(list(have), 3):
+                cnd = a ^ b ^ d
+                if cnd in have:
+                    continue
+                have[cnd] = -1
+                n = sum(1 for m in need if one_op(m))
+                del have[cnd]
+                if n > best_n:
+                    best, best_n, best_src = cnd, n, (have[a], have[b], have[d])
+            done = (best, best_src)
+        m, src = done
+        have[m] = len(vals)
+        vals.append(m)
+        ops.append(src)
+        need = [x for x in need if x not in have]
+    return ops, [have[m] for m in outs_m]
+
+
 def block(K, E, C, R0, NR, T):
     rows = [[mat_row(gf_pow2(r * T), b) for b in range(8)] for r in range(R0, R0 + NR)]
     ops, vals, pair = program({m for row in rows for m in row})
@@ -136,6 +187,20 @@ def main():
                 out.append(f"    static constexpr uint8_t outs[{NR * 8}][2] = {{{w}}};")
                 out.append("};")
     out.append(f"// {nblk} blocks, {total / max(1, nblk):.2f} composite XORs per source on average")
+    # Horner twiddles: row r of a plan with chunk C is multiplied by 2^(C r)
+    tw_total = tw_n = 0
+    for K, E, C, NW in PLANS:
+        for r in range(E):
+            ops, outs = twiddle(gf_pow2(C * r))
+            tw_total += len(ops)
+            tw_n += 1
+            o = ", ".join("{%d, %d, %d}" % op for op in ops) if ops else "{255, 255, 255}"
+            out.append(f"template <> struct TwProg<{K}, {E}, {C}, {r}> {{")
+            out.append(f"    static constexpr int NOPS = {len(ops)};")
+            out.append(f"    static constexpr uint8_t ops[{max(1, len(ops))}][3] = {{{o}}};")
+            out.append(f"    static constexpr uint8_t outs[8] = {{{', '.join(map(str, outs))}}};")
+            out.append("};")
+    out.append(f"// {tw_n} twiddle rows, {tw_total / max(1, tw_n):.2f} XORs per row on average")
     with open(sys.argv[1], "w") as f:
         f.write("\n".join(out) + "\n")
 

@@ -45,44 +45,8 @@
 namespace rsgpu {
 namespace bs {
 
-// row b of the 8x8 GF(2) matrix of "multiply by c": bit a set iff bit b of
-// c * 2^a is set (column a = c * 2^a, computed by doubling)
-constexpr uint8_t mat_row(uint8_t c, int b)
-{
-    uint8_t row = 0;
-    uint8_t v = c;
-    for (int a = 0; a < 8; ++a) {
-        if ((v >> b) & 1)
-            row |= (uint8_t)(1u << a);
-        v = (uint8_t)((v << 1) ^ ((v & 0x80) ? 0x1D : 0));
-    }
-    return row;
-}
-
 template <int K, int E, int C>
-struct Plan {
-    // the per-source coefficients 2^(r t), t < C, are compiled into the XOR
-    // programs of gen_enc_progs.py (EncProg below); the plan keeps the
-    // Horner twiddles
-    uint8_t tw[E][8];  // rows of 2^(C r)
-    constexpr Plan() : tw()
-    {
-        uint8_t g = 1;  // 2^r
-        for (int r = 0; r < E; ++r) {
-            uint8_t v = 1;  // 2^(r t)
-            for (int t = 0; t < C; ++t)
-                v = gf_mul_slow(v, g);
-            // v == 2^(r C) now
-            for (int b = 0; b < 8; ++b)
-                tw[r][b] = mat_row(v, b);
-            g = gf_mul_slow(g, 2);
-        }
-    }
-};
-
-template <int K, int E, int C>
-struct PlanHolder {
-    static constexpr Plan<K, E, C> p{};
+struct PlanHolder {  // the code (K, E) and its Horner chunk C
     static constexpr int k = K, e = E, c = C;
 };
 
@@ -92,38 +56,27 @@ struct PlanHolder {
 // plane the one or two values it adds.
 template <int K, int E, int C, int R0, int NR, int T>
 struct EncProg;
+template <int K, int E, int C, int R>
+struct TwProg;
 #include "enc_progs.inc"
 
-// XOR of the accumulator planes selected by MASK (the Horner twiddles)
-template <int MASK>
-__device__ __forceinline__ uint32_t xsel(const uint32_t (&v)[8])
-{
-    uint32_t t[8];
-    int n = 0;
-#pragma unroll
-    for (int a = 0; a < 8; ++a)
-        if ((MASK >> a) & 1)
-            t[n++] = v[a];
-    if (n == 0)
-        return 0;
-    uint32_t s = t[0];
-    int i = 1;
-    while (i + 1 < n) {
-        s = x3(s, t[i], t[i + 1]);
-        i += 2;
-    }
-    if (i < n)
-        s ^= t[i];
-    return s;
-}
+template <class PR, int I, int NV>
+__device__ __forceinline__ void prog_op(uint32_t (&V)[NV]);
 
+// row R's accumulator times 2^(C R): the generated XOR program over its 8
+// planes (TwProg, gen_enc_progs.py)
 template <class P, int R, int... Bs>
 __device__ __forceinline__ void twiddle_row(uint32_t (&acc)[8], std::integer_sequence<int, Bs...>)
 {
-    uint32_t o[8] = {xsel<P::p.tw[R][Bs]>(acc)...};
+    using PR = TwProg<P::k, P::e, P::c, R>;
+    uint32_t V[8 + PR::NOPS];
 #pragma unroll
-    for (int b = 0; b < 8; ++b)
-        acc[b] = o[b];
+    for (int a = 0; a < 8; ++a)
+        V[a] = acc[a];
+    [&]<int... Is>(std::integer_sequence<int, Is...>) {
+        (prog_op<PR, Is>(V), ...);
+    }(std::make_integer_sequence<int, PR::NOPS>{});
+    ((acc[Bs] = V[PR::outs[Bs]]), ...);
 }
 
 template <class P, int R0, int NR, int... Rs>

@@ -249,3 +249,25 @@ def test_encode_programs_cover_every_output():
                     assert got == ge.mat_row(ge.gf_pow2(r * T), b), (K, E, C, R0, T, o)
                 nblk += 1
     assert nblk == 233
+
+
+def test_twiddle_programs():
+    """The Horner twiddle programs of k_rs_bs (row r times 2^(C r), one per
+    row of every plan), evaluated symbolically over the 8 accumulator planes."""
+    n = 0
+    for K, E, C, NW in ge.PLANS:
+        for r in range(E):
+            c = ge.gf_pow2(C * r)
+            ops, outs = ge.twiddle(c)
+            V = [1 << a for a in range(8)]
+            for op in ops:
+                assert all(i < len(V) or i == ge.NONE for i in op)
+                x = 0
+                for i in op:
+                    if i != ge.NONE:
+                        x ^= V[i]
+                V.append(x)
+            for b in range(8):
+                assert V[outs[b]] == ge.mat_row(c, b), (K, E, C, r, b)
+            n += 1
+    assert n == sum(E for _, E, _, _ in ge.PLANS)
