@@ -163,9 +163,10 @@ def chunk(nt: int) -> list:
             if t + 1 < nt:  # the other plane set is idle: read one source ahead
                 ins += sload(t + 1, nxt) + stage(t + 1, PB if t % 2 == 0 else STAGE)
             ins += tables(t & 1)
-            ins.append("s_set_gpr_idx_on 0, gpr_idx(SRC0,DST)")
-            for slot in range(8):
-                if slot:
+            for slot in range(8):  # slot 0 outside index mode (no relocation)
+                if slot == 1:
+                    ins.append("s_set_gpr_idx_on 8, gpr_idx(SRC0,DST)")
+                elif slot > 1:
                     ins.append(f"s_set_gpr_idx_idx {8 * slot}")
                 ins.append(f"s_swappc_b64 s[{RET}:{RET + 1}], s[{cur + 2 * slot}:{cur + 2 * slot + 1}]")
             ins.append("s_set_gpr_idx_off")
@@ -188,17 +189,21 @@ def chunk(nt: int) -> list:
             for slot in range(8):
                 ins += mac_lines(0x53 + 16 * slot, slot)
         elif CHAIN:
-            ins.append("s_set_gpr_idx_on 0, gpr_idx(SRC0,DST)")
+            # pair 0 (slots 0 and 1) needs no relocation: it runs before index
+            # mode is switched on, so its 16 VALU escape the index-mode cost
             for p in range(4):
-                if p:
+                if p == 1:
+                    ins.append("s_set_gpr_idx_on 16, gpr_idx(SRC0,DST)")
+                elif p > 1:
                     ins.append(f"s_set_gpr_idx_idx {16 * p}")
                 ins.append(f"s_mov_b64 s[{RA}:{RA + 1}], s[{cur + 4 * p + 2}:{cur + 4 * p + 3}]")
                 ins.append(f"s_swappc_b64 s[{RET}:{RET + 1}], s[{cur + 4 * p}:{cur + 4 * p + 1}]")
             ins.append("s_set_gpr_idx_off")
         else:
-            ins.append("s_set_gpr_idx_on 0, gpr_idx(SRC0,DST)")
-            for slot in range(8):
-                if slot:
+            for slot in range(8):  # slot 0 outside index mode (no relocation)
+                if slot == 1:
+                    ins.append("s_set_gpr_idx_on 8, gpr_idx(SRC0,DST)")
+                elif slot > 1:
                     ins.append(f"s_set_gpr_idx_idx {8 * slot}")
                 ins.append(f"s_swappc_b64 s[{RET}:{RET + 1}], s[{cur + 2 * slot}:{cur + 2 * slot + 1}]")
             ins.append("s_set_gpr_idx_off")

@@ -175,7 +175,7 @@ def test_chunk_dispatch(nt):
                 sregs[base + 2 * s] = coef[t][s]
             continue
         if i.startswith("s_set_gpr_idx_on"):
-            idx = 0
+            idx = int(i.split()[1].rstrip(","))
         elif i.startswith("s_set_gpr_idx_idx"):
             idx = int(i.split()[1])
         elif i.startswith("s_set_gpr_idx_off"):
@@ -184,7 +184,7 @@ def test_chunk_dispatch(nt):
             m = SMOV.match(i)
             sregs[int(m.group(1))] = sregs[int(m.group(2))]
         elif i.startswith("s_swappc"):
-            assert idx is not None
+            rel = idx or 0  # outside index mode the handler registers are absolute
             reg = int(SWAP.match(i).group(1))
             # dbuf layout: the handler copy follows the source parity, i.e.
             # which address bank the chunk dispatches from
@@ -195,9 +195,9 @@ def test_chunk_dispatch(nt):
                     if h.startswith("s_"):
                         continue
                     mm = INSN.match(h)
-                    op, d = mm.group(1), int(mm.group(2)) + idx
+                    op, d = mm.group(1), int(mm.group(2)) + rel
                     ops = [int(x) for x in mm.groups()[2:] if x]
-                    ops[0] += idx  # gpr_idx(SRC0,DST)
+                    ops[0] += rel  # gpr_idx(SRC0,DST)
                     val = 0
                     for o in ops:
                         val ^= regs[o]
