@@ -33,36 +33,24 @@ STRIDE = 72  # 8 x 8-byte VOP3 + s_setpc_b64 (4) + s_nop pad (4)
 # staging copies); the 11 composite L entries follow at v32.., then the 11 H.
 # "staged" layout (RSGPU_TC_LAYOUT=staged): L[n] = v[31 + n], H[n] = v[46 + n],
 # planes read one source ahead into v24..v31 and copied in (8 v_mov).
-# "dbuf" (RSGPU_TC_LAYOUT=dbuf, experiment): two plane sets, v24..v31 and
-# v54..v61, used by alternate sources, so the next source's planes are read
-# one source ahead without copies; a second handler copy reads set B (the
-# copy is chosen by SOURCE parity, so the slot-pair chain is off).
 LAYOUT = os.environ.get("RSGPU_TC_LAYOUT", "late")
-assert LAYOUT in ("late", "staged", "dbuf"), LAYOUT
-PB = 54  # plane set B of the dbuf layout
+assert LAYOUT in ("late", "staged"), LAYOUT
 _COMPOSITE = [n for n in range(1, 16) if n & (n - 1)]
 
 
-def reg_l(n: int, pset: int = 0) -> int:
+def reg_l(n: int) -> int:
     if LAYOUT == "staged":
         return 31 + n
-    single = n & (n - 1) == 0
-    if single and pset:
-        return PB + (n.bit_length() - 1)
-    return 24 + (n.bit_length() - 1) if single else 32 + _COMPOSITE.index(n)
+    return 24 + (n.bit_length() - 1) if n & (n - 1) == 0 else 32 + _COMPOSITE.index(n)
 
 
-def reg_h(n: int, pset: int = 0) -> int:
+def reg_h(n: int) -> int:
     if LAYOUT == "staged":
         return 46 + n
-    single = n & (n - 1) == 0
-    if single and pset:
-        return PB + 4 + (n.bit_length() - 1)
-    return 28 + (n.bit_length() - 1) if single else 43 + _COMPOSITE.index(n)
+    return 28 + (n.bit_length() - 1) if n & (n - 1) == 0 else 43 + _COMPOSITE.index(n)
 
 
-TABLE_REGS = sorted({reg_l(n) for n in range(1, 16)} | {reg_h(n) for n in range(1, 16)} |
-                    (set(range(PB, PB + 8)) if LAYOUT == "dbuf" else set()))
+TABLE_REGS = sorted({reg_l(n) for n in range(1, 16)} | {reg_h(n) for n in range(1, 16)})
 
 
 def gf_mul(a: int, b: int) -> int:
@@ -85,22 +73,43 @@ def mat_row(c: int, b: int) -> int:
     return row
 
 
-# Chained dispatch (default; RSGPU_TC_CHAIN=0 for call/return per slot): a
-# second copy of the handlers serves the odd slot of each slot pair.  An even
-# handler works on slot 2p (v[ACC..] relocated by 16p) and jumps straight to
-# the odd handler whose address the chunk put in s[RA:RA+1]; the odd handler
-# works on slot 2p+1 (v[ACC+8..], same relocation) and returns.  Three jumps
-# and five SALU per slot pair instead of four and six.
-CHAIN = os.environ.get("RSGPU_TC_CHAIN", "1") == "1" and LAYOUT != "dbuf"
-NHANDLERS = 512 if CHAIN or LAYOUT == "dbuf" else 256
-RA = 80  # s[80:81]; s[100:101] would be a reserved pair on gfx950
+# Chained dispatch.  RSGPU_TC_CHAIN = number of handler copies (default 2):
+# copy k works on v[ACC + 8k ..] and, except the last copy, continues at the
+# address the chunk put in s[RA_LIST[k]] (the next slot's handler) instead of
+# returning; the last copy returns.  With GPR indexing relocating a whole
+# group by one index, a group of slots costs one s_swappc, one jump per
+# further slot and one return.  1 = call/return per slot; 2 = slot pairs
+# (3 jumps, 5 SALU per pair); 3 = triples (slots 0-2, 3-5 and 6-7).  A group
+# at index 0 runs before index mode is switched on: GPR index mode costs
+# every VALU instruction it covers about one issue cycle
+# (tools/ubench_idx.hip), and these slots need no relocation.
+CHAIN = int(os.environ.get("RSGPU_TC_CHAIN", "2") or "1")
+CHAIN = 1 if CHAIN == 0 else CHAIN
+assert CHAIN in (1, 2, 3), CHAIN
+NCOPY = CHAIN
+NHANDLERS = 256 * NCOPY
+RA_LIST = [80, 60][: NCOPY - 1]  # s[80:81], s[60:61]; s[100:101] is reserved on gfx950
+# dispatch groups: (first slot, handler copy of each slot, GPR index)
+if NCOPY == 1:
+    GROUPS = [(sl, [0], 8 * sl) for sl in range(8)]
+elif NCOPY == 2:
+    GROUPS = [(2 * p, [0, 1], 16 * p) for p in range(4)]
+else:
+    GROUPS = [(0, [0, 1, 2], 0), (3, [0, 1, 2], 24), (6, [1, 2], 40)]
+SLOT_COPY = [0] * 8
+for _s0, _ks, _ix in GROUPS:
+    assert _ks[-1] == NCOPY - 1  # a group ends with the returning copy
+    for _i, _k in enumerate(_ks):
+        SLOT_COPY[_s0 + _i] = _k
+        assert 8 * (_s0 + _i) == 8 * _k + _ix  # one index relocates the group
+RA = RA_LIST[0] if RA_LIST else None
 
 
-def handler(c: int, odd: bool = False) -> list:
-    """Handler of coefficient c; `odd` = the odd-slot copy of chained mode."""
-    ret = RA if CHAIN and not odd else RET
-    base = ACC + 8 if CHAIN and odd else ACC
-    ps = 1 if LAYOUT == "dbuf" and odd else 0
+def handler(c: int, copy: int = 0) -> list:
+    """Handler of coefficient c, handler copy `copy` (chained dispatch)."""
+    copy = int(copy)
+    ret = RA_LIST[copy] if copy < NCOPY - 1 else RET
+    base = ACC + 8 * copy
     if c == 0:
         # no-op: continue at once; pad to STRIDE with never-executed s_nop
         return [f"s_setpc_b64 s[{ret}:{ret + 1}]"] + ["s_nop 0"] * ((STRIDE - 4) // 4)
@@ -110,11 +119,11 @@ def handler(c: int, odd: bool = False) -> list:
         lo, hi = m & 15, m >> 4
         acc = base + b
         if lo and hi:
-            ins.append(f"v_bitop3_b32 v{acc}, v{acc}, v{reg_l(lo, ps)}, v{reg_h(hi, ps)} bitop3:0x96")
+            ins.append(f"v_bitop3_b32 v{acc}, v{acc}, v{reg_l(lo)}, v{reg_h(hi)} bitop3:0x96")
         elif lo:
-            ins.append(f"v_xor_b32_e64 v{acc}, v{acc}, v{reg_l(lo, ps)}")
+            ins.append(f"v_xor_b32_e64 v{acc}, v{acc}, v{reg_l(lo)}")
         elif hi:
-            ins.append(f"v_xor_b32_e64 v{acc}, v{acc}, v{reg_h(hi, ps)}")
+            ins.append(f"v_xor_b32_e64 v{acc}, v{acc}, v{reg_h(hi)}")
         else:  # a nonzero c has an invertible matrix: no zero rows
             raise AssertionError("zero row for nonzero coefficient")
     ins.append(f"s_setpc_b64 s[{ret}:{ret + 1}]")
@@ -123,10 +132,9 @@ def handler(c: int, odd: bool = False) -> list:
 
 
 def handler_table() -> list:
-    """All handlers in address order: c = 0..255 (even / only copy), then in
-    chained mode the odd copy.  Handler number h lives at base + h * STRIDE."""
-    return [i for odd in ((False, True) if NHANDLERS == 512 else (False,)) for c in range(256)
-            for i in handler(c, odd)]
+    """All handlers in address order: copy 0's c = 0..255, then copy 1's, ...
+    Handler (copy k, coefficient c) lives at base + (256 k + c) * STRIDE."""
+    return [i for k in range(NCOPY) for c in range(256) for i in handler(c, k)]
 
 
 PLANE_REG = [reg_l(1), reg_l(2), reg_l(4), reg_l(8), reg_h(1), reg_h(2), reg_h(4), reg_h(8)]
@@ -155,24 +163,6 @@ def chunk(nt: int) -> list:
         off = "0" if t == 0 else f"%[o{t}]"
         return [f"s_load_dwordx16 s[{bank}:{bank + 15}], %[pa], {off}"]
 
-    if LAYOUT == "dbuf":
-        ins = [f"s_mov_b32 s{SM0}, m0"] + sload(0, BANK[0]) + stage(0, STAGE)
-        for t in range(nt):
-            cur, nxt = BANK[t & 1], BANK[(t + 1) & 1]
-            ins.append("s_waitcnt lgkmcnt(0)")
-            if t + 1 < nt:  # the other plane set is idle: read one source ahead
-                ins += sload(t + 1, nxt) + stage(t + 1, PB if t % 2 == 0 else STAGE)
-            ins += tables(t & 1)
-            for slot in range(8):  # slot 0 outside index mode (no relocation)
-                if slot == 1:
-                    ins.append("s_set_gpr_idx_on 8, gpr_idx(SRC0,DST)")
-                elif slot > 1:
-                    ins.append(f"s_set_gpr_idx_idx {8 * slot}")
-                ins.append(f"s_swappc_b64 s[{RET}:{RET + 1}], s[{cur + 2 * slot}:{cur + 2 * slot + 1}]")
-            ins.append("s_set_gpr_idx_off")
-        ins += [f"s_mov_b32 m0, s{SM0}", "s_nop 0"]
-        return ins
-
     late = LAYOUT == "late"
     ins = [f"s_mov_b32 s{SM0}, m0"] + sload(0, BANK[0]) + stage(0)
     for t in range(nt):
@@ -188,25 +178,20 @@ def chunk(nt: int) -> list:
         if os.environ.get("RSGPU_TC_FAKE") == "inline":  # timing experiment only: wrong products
             for slot in range(8):
                 ins += mac_lines(0x53 + 16 * slot, slot)
-        elif CHAIN:
-            # pair 0 (slots 0 and 1) needs no relocation: it runs before index
-            # mode is switched on, so its 16 VALU escape the index-mode cost
-            for p in range(4):
-                if p == 1:
-                    ins.append("s_set_gpr_idx_on 16, gpr_idx(SRC0,DST)")
-                elif p > 1:
-                    ins.append(f"s_set_gpr_idx_idx {16 * p}")
-                ins.append(f"s_mov_b64 s[{RA}:{RA + 1}], s[{cur + 4 * p + 2}:{cur + 4 * p + 3}]")
-                ins.append(f"s_swappc_b64 s[{RET}:{RET + 1}], s[{cur + 4 * p}:{cur + 4 * p + 1}]")
-            ins.append("s_set_gpr_idx_off")
         else:
-            for slot in range(8):  # slot 0 outside index mode (no relocation)
-                if slot == 1:
-                    ins.append("s_set_gpr_idx_on 8, gpr_idx(SRC0,DST)")
-                elif slot > 1:
-                    ins.append(f"s_set_gpr_idx_idx {8 * slot}")
-                ins.append(f"s_swappc_b64 s[{RET}:{RET + 1}], s[{cur + 2 * slot}:{cur + 2 * slot + 1}]")
-            ins.append("s_set_gpr_idx_off")
+            mode = False
+            for s0, ks, ix in GROUPS:
+                if ix and not mode:
+                    ins.append(f"s_set_gpr_idx_on {ix}, gpr_idx(SRC0,DST)")
+                    mode = True
+                elif ix:
+                    ins.append(f"s_set_gpr_idx_idx {ix}")
+                for i in range(1, len(ks)):  # continuations of the chain
+                    ra, sl = RA_LIST[ks[i - 1]], s0 + i
+                    ins.append(f"s_mov_b64 s[{ra}:{ra + 1}], s[{cur + 2 * sl}:{cur + 2 * sl + 1}]")
+                ins.append(f"s_swappc_b64 s[{RET}:{RET + 1}], s[{cur + 2 * s0}:{cur + 2 * s0 + 1}]")
+            if mode:
+                ins.append("s_set_gpr_idx_off")
         if late and t + 1 < nt:  # the planes are free once the dispatch is done
             ins += stage(t + 1)
     ins += [f"s_mov_b32 m0, s{SM0}", "s_nop 0"]
@@ -246,14 +231,14 @@ def mac_lines(c: int, slot: int) -> list:
     return ins
 
 
-def tables(pset: int = 0) -> list:
-    """The 22 composite entries from plane set `pset` (dbuf layout: 1 = B)."""
+def tables() -> list:
+    """The 22 composite entries of the four-Russians tables."""
     ins = []
     for reg in (reg_l, reg_h):
         for n in range(1, 16):
             low = n & -n
             if n != low:
-                ins.append(f"v_xor_b32_e32 v{reg(n)}, v{reg(n ^ low, pset)}, v{reg(low, pset)}")
+                ins.append(f"v_xor_b32_e32 v{reg(n)}, v{reg(n ^ low)}, v{reg(low)}")
     return ins
 
 
@@ -386,7 +371,7 @@ def main() -> None:
         f"#define RSGPU_TC_ACC {ACC}",
         f"#define RSGPU_TC_LAYOUT_{LAYOUT.upper()} 1",
         f"#define RSGPU_TC_NHANDLERS {NHANDLERS}",
-        f"#define RSGPU_TC_COPY_BY_SOURCE {1 if LAYOUT == 'dbuf' else 0}",
+        "#define RSGPU_TC_SLOT_COPY {" + ", ".join(map(str, SLOT_COPY)) + "}",
         f"#define RSGPU_TC_RET {RET}",
         "#define RSGPU_TC_HANDLERS \\",
     ]
@@ -418,8 +403,8 @@ def main() -> None:
     lines.append("#define RSGPU_TC_ACC_CLOBBERS " + ", ".join(f'"v{ACC + i}"' for i in range(64)))
     vclob = sorted(set(range(STAGE, STAGE + 8)) | set(TABLE_REGS))
     sclob = list(range(BANK[0], BANK[0] + 16)) + [SM0, RET, RET + 1] + list(range(BANK[1], BANK[1] + 16))
-    if CHAIN:
-        sclob += [RA, RA + 1]
+    for ra in RA_LIST:
+        sclob += [ra, ra + 1]
     lines.append("#define RSGPU_TC_CLOBBERS " + ", ".join(
         [f'"v{r}"' for r in vclob] + [f'"s{r}"' for r in sclob] + ['"scc"']))
     lines.append("")

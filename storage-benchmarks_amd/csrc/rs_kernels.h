@@ -107,11 +107,12 @@ hipError_t launch_rs_decode_fused(int k, int e, const uint8_t* src, const uint8_
                                   const unsigned long long* syn_addr, const int* status,
                                   hipStream_t st);
 int tc_handler_stride();
-// handlers in the table: 256, or 512 with the chained dispatch's odd-slot
-// copy at 256..511.  Consumers index the context's 512-entry address table
-// as tc_table[(slot & 1) * 256 + c] (its upper half repeats the lower one
-// when there is no odd copy).
+// handlers in the table (256 per handler copy of the chained dispatch) and
+// the copy serving slot s (0..7).  Consumers index the context's 2048-entry
+// address table as tc_table[(slot & 7) * 256 + c]: the address of handler
+// (tc_slot_copy(slot), c).
 int tc_handler_count();
+int tc_slot_copy(int slot);
 hipError_t tc_query_handlers(unsigned long long* d_out, hipStream_t st);
 hipError_t launch_rs_tc(const TcArgs& a, long long blocks, hipStream_t st);
 

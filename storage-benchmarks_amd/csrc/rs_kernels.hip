@@ -498,11 +498,11 @@ __global__ __launch_bounds__(256) void k_decode_prepare(int k, int e, int rows_p
     if (tc_addr && tc_table) {
         // k_rs_tc handler addresses [j][slot]: coefficient inv(b)[err[slot]][j]
         // of survivor j (the isa.cpp:184-204 decode rows), padding slots ->
-        // handler 0; the table is [slot parity][coefficient]
+        // handler 0; the table is [slot][coefficient]
         unsigned long long* ta = tc_addr + (size_t)b * k * tc_rows;
         for (int idx = tid; idx < k * tc_rows; idx += nt) {
             const int j = idx / tc_rows, r = idx - j * tc_rows;
-            ta[idx] = tc_table[(r & 1) * 256 + (r < e ? Dm[eb[r] * k + j] : 0)];
+            ta[idx] = tc_table[(r & 7) * 256 + (r < e ? Dm[eb[r] * k + j] : 0)];
         }
         return;
     }
@@ -961,7 +961,7 @@ __global__ __launch_bounds__(256) void k_decode_prepare_syn(int k, int e, int ro
                     c = A[i * e + (q - nl)];
                 }
             }
-            da[idx] = tc_table[(i & 1) * 256 + c];
+            da[idx] = tc_table[(i & 7) * 256 + c];
         }
         return;
     }
@@ -1061,7 +1061,7 @@ __global__ __launch_bounds__(256) void k_decode_prepare_syn(int k, int e, int ro
         unsigned long long* sa = syn_addr + (size_t)b * (k - e) * tc_rows;
         for (int idx = tid; idx < (k - e) * tc_rows; idx += nt) {
             const int q = idx / tc_rows, r = idx - q * tc_rows;
-            sa[idx] = tc_table[(r & 1) * 256 + (r < e ? gexp[(r * (int)lv[q]) % 255] : 0)];
+            sa[idx] = tc_table[(r & 7) * 256 + (r < e ? gexp[(r * (int)lv[q]) % 255] : 0)];
         }
     }
     if (tc_addr) {
@@ -1070,7 +1070,7 @@ __global__ __launch_bounds__(256) void k_decode_prepare_syn(int k, int e, int ro
         unsigned long long* ta = tc_addr + (size_t)b * e * tc_rows;
         for (int idx = tid; idx < e * tc_rows; idx += nt) {
             const int p = idx / tc_rows, i = idx - p * tc_rows;
-            ta[idx] = tc_table[(i & 1) * 256 + (i < e ? Dm[i * n + p] : 0)];
+            ta[idx] = tc_table[(i & 7) * 256 + (i < e ? Dm[i * n + p] : 0)];
         }
     }
     if (!tabs4)

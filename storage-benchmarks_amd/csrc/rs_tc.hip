@@ -284,6 +284,12 @@ int tc_handler_stride() { return RSGPU_TC_STRIDE; }
 
 int tc_handler_count() { return RSGPU_TC_NHANDLERS; }
 
+int tc_slot_copy(int slot)
+{
+    static constexpr int copy[8] = RSGPU_TC_SLOT_COPY;
+    return copy[slot & 7];
+}
+
 int tc_rows_per_pass(int rows) { return rows <= 0 ? 8 : (rows + 7) / 8 * 8; }
 
 hipError_t launch_rs_tc(const TcArgs& a, long long blocks, hipStream_t st)

@@ -27,7 +27,7 @@ struct rsgpu_ctx {
     // threaded-code solve (rs_tc.hip): device table of the 256 handler
     // addresses; tc_state 0 = not probed, 1 = ready, -1 = unavailable
     unsigned long long* d_tc_table = nullptr;
-    unsigned long long h_tc_table[512] = {};  // [slot parity][coefficient]
+    unsigned long long h_tc_table[2048] = {};  // [slot][coefficient]
     int tc_state = 0;
     std::string err;
     // grow-only device scratch for pointer tables / coefficient tables
@@ -688,33 +688,35 @@ int rsgpu_encode_blocks(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch, 
 // reports the table's first and end addresses; the layout must be exactly
 // tc_handler_count() handlers of tc_handler_stride() bytes, otherwise the
 // threaded-code path stays off (and k_dot_generic solves).  The address
-// table has 512 entries: [slot parity][coefficient].
+// table has 2048 entries: [slot][coefficient], each the handler copy that
+// serves the slot (tc_slot_copy).
 static int tc_init(rsgpu_ctx* ctx)
 {
     if (ctx->tc_state != 0)
         return ctx->tc_state;
     ctx->tc_state = -1;
     unsigned long long* d = nullptr;
-    if (hipMalloc((void**)&d, 514 * sizeof(unsigned long long)) != hipSuccess)
+    if (hipMalloc((void**)&d, 2050 * sizeof(unsigned long long)) != hipSuccess)
         return -1;
     unsigned long long se[2] = {0, 0};
-    if (tc_query_handlers(d + 512, ctx->stream) != hipSuccess ||
-        hipMemcpyAsync(se, d + 512, sizeof se, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
+    if (tc_query_handlers(d + 2048, ctx->stream) != hipSuccess ||
+        hipMemcpyAsync(se, d + 2048, sizeof se, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
         hipStreamSynchronize(ctx->stream) != hipSuccess) {
         (void)hipFree(d);
         return -1;
     }
     const unsigned long long stride = (unsigned long long)tc_handler_stride();
     const unsigned long long count = (unsigned long long)tc_handler_count();
-    if (se[0] == 0 || se[1] - se[0] != count * stride || (count != 256 && count != 512)) {
+    if (se[0] == 0 || se[1] - se[0] != count * stride || count % 256 != 0 || count > 2048) {
         std::fprintf(stderr, "rsgpu: threaded-code handler table has an unexpected layout "
                              "(%#llx..%#llx); using k_dot_generic\n", se[0], se[1]);
         (void)hipFree(d);
         return -1;
     }
-    unsigned long long h[512];
-    for (int c = 0; c < 512; ++c)
-        h[c] = se[0] + (unsigned long long)(count == 512 ? c : c & 255) * stride;
+    unsigned long long h[2048];
+    for (int s = 0; s < 8; ++s)
+        for (int c = 0; c < 256; ++c)
+            h[s * 256 + c] = se[0] + (unsigned long long)(tc_slot_copy(s) * 256 + c) * stride;
     if (hipMemcpy(d, h, sizeof h, hipMemcpyHostToDevice) != hipSuccess) {
         (void)hipFree(d);
         return -1;
@@ -737,7 +739,7 @@ void tc_fill_addr(const rsgpu_ctx* ctx, const uint8_t* coef, int k, int rows, un
     const int slots = tc_rows_per_pass(rows);
     for (int j = 0; j < k; ++j)
         for (int s = 0; s < slots; ++s)
-            h[(size_t)j * slots + s] = ctx->h_tc_table[(s & 1) * 256 + (s < rows ? coef[(size_t)s * k + j] : 0)];
+            h[(size_t)j * slots + s] = ctx->h_tc_table[(s & 7) * 256 + (s < rows ? coef[(size_t)s * k + j] : 0)];
 }
 
 int tc_launch_shared(rsgpu_ctx* ctx, const unsigned long long* d_addr, int k, int rows, long long len,

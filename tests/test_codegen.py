@@ -45,31 +45,30 @@ def unplanes(p):
     return [sum(((p[a] >> i) & 1) << a for a in range(8)) for i in range(32)]
 
 
-def load_tables(regs, by, pset=0):
-    """The four-Russians tables of one source: single-bit entries = planes
-    (plane set `pset` of the dbuf layout), the rest built by the generator's
-    own table code."""
+def load_tables(regs, by):
+    """The four-Russians tables of one source: single-bit entries = planes,
+    the rest built by the generator's own table code."""
     p = planes(by)
-    for a in range(8):
-        regs[(g.reg_l if a < 4 else g.reg_h)(1 << (a % 4), pset)] = p[a]
-    run(g.tables(pset), regs)
+    for a, r in enumerate(g.PLANE_REG):
+        regs[r] = p[a]
+    run(g.tables(), regs)
 
 
 @pytest.mark.parametrize("c", range(256))
 def test_handler_multiplies(c):
-    for odd in (False, True):
+    for copy in range(g.NCOPY):
         rng = random.Random(c)
         regs = {i: 0 for i in range(256)}
         src = [rng.randrange(256) for _ in range(32)]
         acc = [rng.randrange(256) for _ in range(32)]
-        load_tables(regs, src, 1 if g.LAYOUT == "dbuf" and odd else 0)
-        base = g.ACC + (8 if g.CHAIN and odd else 0)
+        load_tables(regs, src)
+        base = g.ACC + 8 * copy
         for a, v in enumerate(planes(acc)):
             regs[base + a] = v
-        body = g.handler(c, odd)
+        body = g.handler(c, copy)
         assert sum(4 if i.startswith("s_") else 8 for i in body) == g.STRIDE
-        # even copy of chained mode continues at s[RA], everything else returns
-        ret = g.RA if g.CHAIN and not odd else g.RET
+        # copies before the last continue the chain, the last one returns
+        ret = g.RA_LIST[copy] if copy < g.NCOPY - 1 else g.RET
         assert f"s_setpc_b64 s[{ret}:{ret + 1}]" in body
         run(body, regs)
         got = unplanes([regs[base + a] for a in range(8)])
@@ -172,7 +171,7 @@ def test_chunk_dispatch(nt):
             base, off = int(m.group(1)), m.group(3)
             t = 0 if off == "0" else int(off[3:-1])
             for s in range(8):
-                sregs[base + 2 * s] = coef[t][s]
+                sregs[base + 2 * s] = (s, coef[t][s])
             continue
         if i.startswith("s_set_gpr_idx_on"):
             idx = int(i.split()[1].rstrip(","))
@@ -185,12 +184,10 @@ def test_chunk_dispatch(nt):
             sregs[int(m.group(1))] = sregs[int(m.group(2))]
         elif i.startswith("s_swappc"):
             rel = idx or 0  # outside index mode the handler registers are absolute
-            reg = int(SWAP.match(i).group(1))
-            # dbuf layout: the handler copy follows the source parity, i.e.
-            # which address bank the chunk dispatches from
-            c, odd = sregs[reg], g.LAYOUT == "dbuf" and g.BANK[1] <= reg < g.BANK[1] + 16
-            while True:  # a handler, and in chained mode the one it jumps to
-                body = g.handler(c, odd)
+            slot, c = sregs[int(SWAP.match(i).group(1))]
+            copy = g.SLOT_COPY[slot]  # the prepared address names this copy
+            while True:  # a handler, and in chained mode the ones it jumps to
+                body = g.handler(c, copy)
                 for h in body:
                     if h.startswith("s_"):
                         continue
@@ -205,10 +202,12 @@ def test_chunk_dispatch(nt):
                     regs[d] = val
                 tgt = int(SETPC.search(" ".join(body)).group(1))
                 if tgt == g.RET:
+                    assert copy == g.NCOPY - 1
                     break
-                assert g.LAYOUT != "dbuf"
-                assert g.CHAIN and tgt == g.RA and not odd
-                c, odd = sregs[g.RA], True
+                assert tgt == g.RA_LIST[copy]
+                slot, c = sregs[tgt]
+                assert g.SLOT_COPY[slot] == copy + 1
+                copy += 1
         elif not i.startswith("s_"):
             assert idx is None, i
             run([i], regs)

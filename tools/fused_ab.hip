@@ -73,13 +73,8 @@ int main(int argc, char** argv)
     auto table = [&](size_t n) {
         std::vector<unsigned long long> v(n);
         for (size_t i = 0; i < n; ++i) {  // the handler copy of slot / source parity
-#if RSGPU_TC_COPY_BY_SOURCE
-            const bool odd = (i / 32 % k) & 1;  // dbuf layout: copy by source parity
-#else
-            const bool odd = i & 1;             // chained slot pairs: copy by slot parity
-#endif
-            v[i] = q[0] + (unsigned long long)((tc_handler_count() == 512 && odd ? 256 : 0) +
-                                               1 + rng() % nc) * tc_handler_stride();
+            v[i] = q[0] + (unsigned long long)(tc_slot_copy((int)(i % 8)) * 256 + 1 + rng() % nc) *
+                              tc_handler_stride();
         }
         unsigned long long* d;
         (void)hipMalloc(&d, n * 8);

@@ -51,8 +51,8 @@ int main(int argc, char** argv)
         return 1;
     }
     std::vector<unsigned long long> addr((size_t)B * e * 32);
-    // odd slots use the odd-slot handler copy when the dispatch is chained
-    auto odd = [](size_t i) { return tc_handler_count() == 512 && (i & 1) ? 256ull : 0ull; };
+    // every slot uses the handler copy that serves it (chained dispatch)
+    auto odd = [](size_t i) { return 256ull * tc_slot_copy((int)(i % 8)); };  // the slot's handler copy
     for (size_t i = 0; i < addr.size(); ++i)
         addr[i] = q[0] + (odd(i) + (rng() & 255)) * tc_handler_stride();
     (void)hipMalloc(&d_addr, addr.size() * 8);

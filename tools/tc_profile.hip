@@ -43,9 +43,9 @@ int main(int argc, char** argv)
     const int slots = tc_rows_per_pass(nrows);
     std::vector<unsigned long long> addr((size_t)B * k * slots);
     uint32_t x = 12345;
-    for (size_t i = 0; i < addr.size(); ++i) {  // odd slots: odd-slot copy when chained
+    for (size_t i = 0; i < addr.size(); ++i) {  // the handler copy serving the slot
         x = x * 1664525u + 1013904223u;
-        const unsigned long long h = (tc_handler_count() == 512 && (i & 1) ? 256 : 0) + ((x >> 13) & 255);
+        const unsigned long long h = 256ull * tc_slot_copy((int)(i % 8)) + ((x >> 13) & 255);
         addr[i] = q[0] + h * tc_handler_stride();
     }
     unsigned long long* d_addr;
