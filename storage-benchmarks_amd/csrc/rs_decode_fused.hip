@@ -1,6 +1,13 @@
 // rs_decode_fused.hip -- one-pass syndrome decode for the gf_gen_rs_matrix
 // codes: recovered data rows from the surviving data rows and the parity rows
-// of each block, with HBM traffic (k + e) * L per block (read k, write e).
+// of each block, with HBM traffic (k + e) * L per block (read k, write e)
+// plus the parked syndromes of the waves beyond the LDS hand-off.
+//
+// Status: the default decode is the one-matrix k_rs_tc (rsgpu_capi.cpp
+// decode_mode); this kernel is the default for (k 100, e 20), where it
+// measured 3 % faster, and RSGPU_DECODE=fused selects it elsewhere.  Its
+// phase 1 runs on threaded code by default (TC1 below); the compile-time
+// Horner form described next is kept behind RSGPU_FUSED_SYN=horner.
 //
 // The two-kernel decode (k_rs_bs<SYN> writes the e syndrome rows to HBM,
 // k_rs_tc reads them back and overwrites them with the data) moves 2 e L
