@@ -393,6 +393,10 @@ def main() -> None:
     for slot in range(8):
         body = "".join(f"v_mov_b32 %{q}, v{ACC + 8 * slot + q}\\n" for q in range(8))
         lines.append(f'#define RSGPU_TC_READ_SLOT{slot} "{body}"')
+    for slot in range(8):  # the same with v_mov_b64 into 4 register pairs
+        body = "".join(f"v_mov_b64 %{q}, v[{ACC + 8 * slot + 2 * q}:{ACC + 8 * slot + 2 * q + 1}]\\n"
+                       for q in range(4))
+        lines.append(f'#define RSGPU_TC_READ_SLOT64_{slot} "{body}"')
     for slot in range(8):
         body = "".join(f"v_mov_b32 v{ACC + 8 * slot + q}, %{q}\\n" for q in range(8))
         lines.append(f'#define RSGPU_TC_WRITE_SLOT{slot} "{body}"')

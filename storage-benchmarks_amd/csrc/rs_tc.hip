@@ -119,22 +119,27 @@ __device__ unsigned long long rsgpu_tc_prof[8];
     } while (0)
 #endif
 
-// Read accumulator slot S (asm-owned v[64+8S : 64+8S+7]) into W.
+// Read accumulator slot S (asm-owned v[64+8S : 64+8S+7]) into W, two planes
+// per v_mov_b64.
 template <int S>
 __device__ __forceinline__ void read_slot(uint32_t (&W)[8])
 {
-#define RSGPU_TC_RD(TEXT)                                                                       \
-    asm volatile(TEXT : "=v"(W[0]), "=v"(W[1]), "=v"(W[2]), "=v"(W[3]), "=v"(W[4]), "=v"(W[5]), \
-                        "=v"(W[6]), "=v"(W[7]))
-    if constexpr (S == 0) RSGPU_TC_RD(RSGPU_TC_READ_SLOT0);
-    if constexpr (S == 1) RSGPU_TC_RD(RSGPU_TC_READ_SLOT1);
-    if constexpr (S == 2) RSGPU_TC_RD(RSGPU_TC_READ_SLOT2);
-    if constexpr (S == 3) RSGPU_TC_RD(RSGPU_TC_READ_SLOT3);
-    if constexpr (S == 4) RSGPU_TC_RD(RSGPU_TC_READ_SLOT4);
-    if constexpr (S == 5) RSGPU_TC_RD(RSGPU_TC_READ_SLOT5);
-    if constexpr (S == 6) RSGPU_TC_RD(RSGPU_TC_READ_SLOT6);
-    if constexpr (S == 7) RSGPU_TC_RD(RSGPU_TC_READ_SLOT7);
+    uint64_t P[4];
+#define RSGPU_TC_RD(TEXT) asm volatile(TEXT : "=v"(P[0]), "=v"(P[1]), "=v"(P[2]), "=v"(P[3]))
+    if constexpr (S == 0) RSGPU_TC_RD(RSGPU_TC_READ_SLOT64_0);
+    if constexpr (S == 1) RSGPU_TC_RD(RSGPU_TC_READ_SLOT64_1);
+    if constexpr (S == 2) RSGPU_TC_RD(RSGPU_TC_READ_SLOT64_2);
+    if constexpr (S == 3) RSGPU_TC_RD(RSGPU_TC_READ_SLOT64_3);
+    if constexpr (S == 4) RSGPU_TC_RD(RSGPU_TC_READ_SLOT64_4);
+    if constexpr (S == 5) RSGPU_TC_RD(RSGPU_TC_READ_SLOT64_5);
+    if constexpr (S == 6) RSGPU_TC_RD(RSGPU_TC_READ_SLOT64_6);
+    if constexpr (S == 7) RSGPU_TC_RD(RSGPU_TC_READ_SLOT64_7);
 #undef RSGPU_TC_RD
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        W[2 * q] = (uint32_t)P[q];
+        W[2 * q + 1] = (uint32_t)(P[q] >> 32);
+    }
 }
 
 // amdgpu_num_vgpr(64): the compiler allocates v0..v63 only; the accumulators
