@@ -145,6 +145,11 @@ __device__ __forceinline__ void read_slot(uint32_t (&W)[8])
 // amdgpu_num_vgpr(64): the compiler allocates v0..v63 only; the accumulators
 // v64..v127 are touched by asm alone, so they stay put across the loops (the
 // kernel descriptor still reserves 128 VGPRs because the asm names v127).
+// RSGPU_TC_ONEBAR: one barrier per step (the next step's LDS-DMA issued right
+// after this step's post-transpose barrier) instead of two.
+#ifndef RSGPU_TC_ONEBAR
+#define RSGPU_TC_ONEBAR 1
+#endif
 template <int NW>
 __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_num_vgpr(64))) void k_rs_tc(TcArgs a, int tiles_per_wg)
 {
@@ -204,6 +209,10 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_num_vgpr(64))) void 
         const int nt = min(C, k - ch * C);
         uint4* buf = lds[n & 1];
         TC_PROF_MARK(6);
+#if RSGPU_TC_ONEBAR
+        wait_vm(0);  // this step's own sources, issued behind the previous step's barrier
+        TC_PROF_MARK(0);
+#else
         if (n + 1 < total) {
             issue(n + 1);  // lands while this chunk is transposed and consumed
             TC_PROF_MARK(0);
@@ -211,6 +220,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_num_vgpr(64))) void 
         } else {
             wait_vm(0);
         }
+#endif
         TC_PROF_MARK(1);
         // own share of this chunk: bytes -> bit-planes, in place
         for (int t = wave; t < nt; t += NW) {
@@ -223,6 +233,13 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_num_vgpr(64))) void 
         }
         TC_PROF_MARK(2);
         barrier_lds();
+#if RSGPU_TC_ONEBAR
+        // every wave is past its dispatch of step n - 1, which read buffer
+        // (n + 1) & 1: the next step's sources may land there now and
+        // arrive during this step's dispatch
+        if (n + 1 < total)
+            issue(n + 1);
+#endif
         TC_PROF_MARK(3);
         if (ch == 0)
             asm volatile(RSGPU_TC_ZERO ::: RSGPU_TC_ACC_CLOBBERS);
@@ -271,7 +288,9 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_num_vgpr(64))) void 
             }
         }
         TC_PROF_MARK(5);
+#if !RSGPU_TC_ONEBAR
         barrier_lds();  // buffer n & 1 is refilled by step n + 2
+#endif
     }
     TC_PROF_MARK(6);
     TC_PROF_END;
