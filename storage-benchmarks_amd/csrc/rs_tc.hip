@@ -328,11 +328,16 @@ hipError_t launch_rs_tc(const TcArgs& a, long long blocks, hipStream_t st)
     while (tpw > 1 && ntile * blocks / tpw < 2048)  // keep >= 2048 workgroups
         tpw /= 2;
     dim3 grid((unsigned)((ntile + tpw - 1) / tpw), (unsigned)blocks);
+    // RSGPU_TC_LDS_PAD=bytes: extra dynamic LDS per workgroup, an occupancy
+    // experiment (fewer workgroups per CU); 0 by default
+    unsigned pad = 0;
+    if (const char* v = std::getenv("RSGPU_TC_LDS_PAD"))
+        pad = (unsigned)std::max(0, std::atoi(v));
     switch (nw) {
-    case 1: hipLaunchKernelGGL(tc::k_rs_tc<1>, grid, dim3(64), 0, st, a, tpw); break;
-    case 2: hipLaunchKernelGGL(tc::k_rs_tc<2>, grid, dim3(128), 0, st, a, tpw); break;
-    case 3: hipLaunchKernelGGL(tc::k_rs_tc<3>, grid, dim3(192), 0, st, a, tpw); break;
-    case 4: hipLaunchKernelGGL(tc::k_rs_tc<4>, grid, dim3(256), 0, st, a, tpw); break;
+    case 1: hipLaunchKernelGGL(tc::k_rs_tc<1>, grid, dim3(64), pad, st, a, tpw); break;
+    case 2: hipLaunchKernelGGL(tc::k_rs_tc<2>, grid, dim3(128), pad, st, a, tpw); break;
+    case 3: hipLaunchKernelGGL(tc::k_rs_tc<3>, grid, dim3(192), pad, st, a, tpw); break;
+    case 4: hipLaunchKernelGGL(tc::k_rs_tc<4>, grid, dim3(256), pad, st, a, tpw); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
