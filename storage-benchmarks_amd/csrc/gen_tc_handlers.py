@@ -73,7 +73,7 @@ def mat_row(c: int, b: int) -> int:
     return row
 
 
-# Chained dispatch.  RSGPU_TC_CHAIN = number of handler copies (default 2):
+# Chained dispatch.  RSGPU_TC_CHAIN = number of handler copies (default 3):
 # copy k works on v[ACC + 8k ..] and, except the last copy, continues at the
 # address the chunk put in s[RA_LIST[k]] (the next slot's handler) instead of
 # returning; the last copy returns.  With GPR indexing relocating a whole
@@ -83,7 +83,7 @@ def mat_row(c: int, b: int) -> int:
 # at index 0 runs before index mode is switched on: GPR index mode costs
 # every VALU instruction it covers about one issue cycle
 # (tools/ubench_idx.hip), and these slots need no relocation.
-CHAIN = int(os.environ.get("RSGPU_TC_CHAIN", "2") or "1")
+CHAIN = int(os.environ.get("RSGPU_TC_CHAIN", "3") or "1")
 CHAIN = 1 if CHAIN == 0 else CHAIN
 assert CHAIN in (1, 2, 3), CHAIN
 NCOPY = CHAIN

@@ -13,12 +13,13 @@
 // handler c (RSGPU_TC_STRIDE = 72 bytes, generated) applies coefficient c to
 // an accumulator slot from the four-Russians tables of the current source.
 // Slot s is reached by GPR indexing (s_set_gpr_idx_on / _idx, one index per
-// slot pair), and the handlers chain in slot pairs: the kernel s_swappc's to
-// the even slot's handler, which jumps to the odd slot's handler (a second
-// copy of the 256 working on the next 8 accumulators), which returns.  The 8
-// handler addresses of a source are one s_load_dwordx16 of the table the
-// prepare kernel writes ([source][slot], address of handler copy (slot & 1)
-// for coefficient c).  GPR index mode costs every VALU it covers about one
+// slot group), and the handlers chain in groups of three (slots 0-2, 3-5,
+// 6-7; RSGPU_TC_CHAIN): the kernel s_swappc's to the group's first handler,
+// which jumps to the next slot's handler (another copy of the 256 working on
+// the next 8 accumulators), and the group's last handler returns.  Group 0
+// runs before index mode is switched on.  The 8 handler addresses of a
+// source are one s_load_dwordx16 of the table the prepare kernel writes
+// ([source][slot], address of the slot's handler copy for coefficient c).  GPR index mode costs every VALU it covers about one
 // issue cycle (tools/ubench_idx.hip), the price of reusing one table build
 // for 8 rows without per-slot handler copies.
 //
