@@ -141,13 +141,37 @@ SMOV = re.compile(r"s_mov_b64 s\[(\d+):\d+\], s\[(\d+):\d+\]")
 SETPC = re.compile(r"s_setpc_b64 s\[(\d+):\d+\]")
 
 
+def generator(chain):
+    """gen_tc_handlers imported afresh under RSGPU_TC_CHAIN=chain (its
+    dispatch layout is fixed at import), or the default module for None."""
+    if chain is None:
+        return g
+    import importlib.util
+    old = os.environ.get("RSGPU_TC_CHAIN")
+    os.environ["RSGPU_TC_CHAIN"] = str(chain)
+    try:
+        spec = importlib.util.spec_from_file_location("gen_tc_chain%d" % chain, g.__file__)
+        mod = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(mod)
+    finally:
+        if old is None:
+            del os.environ["RSGPU_TC_CHAIN"]
+        else:
+            os.environ["RSGPU_TC_CHAIN"] = old
+    assert mod.NCOPY == chain
+    return mod
+
+
+@pytest.mark.parametrize("chain", [None, 1, 2, 3], ids=["default", "chain1", "chain2", "chain3"])
 @pytest.mark.parametrize("nt", range(1, g.C + 1))
-def test_chunk_dispatch(nt):
+def test_chunk_dispatch(nt, chain):
     """The per-part chunk asm (gen_tc_handlers.chunk) interpreted with its
     LDS reads, handler-address loads, GPR-index relocation and handler calls:
     every accumulator slot s must end as acc_s ^ sum_t c(t, s) * src_t.  The
     interpreter applies each load at issue, so a read that lands in a register
-    still in use by the dispatch shows up as a wrong product."""
+    still in use by the dispatch shows up as a wrong product.  Every
+    generator chain layout (RSGPU_TC_CHAIN) is checked, not only the built one."""
+    g = generator(chain)
     rng = random.Random(100 + nt)
     src = [[rng.randrange(256) for _ in range(32)] for _ in range(nt)]
     coef = [[rng.randrange(256) for _ in range(8)] for _ in range(nt)]
