@@ -85,17 +85,19 @@ def mat_row(c: int, b: int) -> int:
 # (tools/ubench_idx.hip), and these slots need no relocation.
 CHAIN = int(os.environ.get("RSGPU_TC_CHAIN", "3") or "1")
 CHAIN = 1 if CHAIN == 0 else CHAIN
-assert CHAIN in (1, 2, 3), CHAIN
+assert CHAIN in (1, 2, 3, 4), CHAIN
 NCOPY = CHAIN
 NHANDLERS = 256 * NCOPY
-RA_LIST = [80, 60][: NCOPY - 1]  # s[80:81], s[60:61]; s[100:101] is reserved on gfx950
+RA_LIST = [80, 60, 58][: NCOPY - 1]  # s[80:81], s[60:61], s[58:59]; s[100:101] is reserved on gfx950
 # dispatch groups: (first slot, handler copy of each slot, GPR index)
 if NCOPY == 1:
     GROUPS = [(sl, [0], 8 * sl) for sl in range(8)]
 elif NCOPY == 2:
     GROUPS = [(2 * p, [0, 1], 16 * p) for p in range(4)]
-else:
+elif NCOPY == 3:
     GROUPS = [(0, [0, 1, 2], 0), (3, [0, 1, 2], 24), (6, [1, 2], 40)]
+else:  # 4: quads (72 KB of handlers; an instruction-cache experiment)
+    GROUPS = [(0, [0, 1, 2, 3], 0), (4, [0, 1, 2, 3], 32)]
 SLOT_COPY = [0] * 8
 for _s0, _ks, _ix in GROUPS:
     assert _ks[-1] == NCOPY - 1  # a group ends with the returning copy

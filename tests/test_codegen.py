@@ -162,7 +162,7 @@ def generator(chain):
     return mod
 
 
-@pytest.mark.parametrize("chain", [None, 1, 2, 3], ids=["default", "chain1", "chain2", "chain3"])
+@pytest.mark.parametrize("chain", [None, 1, 2, 3, 4], ids=["default", "chain1", "chain2", "chain3", "chain4"])
 @pytest.mark.parametrize("nt", range(1, g.C + 1))
 def test_chunk_dispatch(nt, chain):
     """The per-part chunk asm (gen_tc_handlers.chunk) interpreted with its
