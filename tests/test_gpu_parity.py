@@ -9,6 +9,7 @@ plus sampled rows against the oracle.
 import hashlib
 import json
 import os
+import sys
 
 import numpy as np
 import pytest
@@ -435,3 +436,14 @@ def test_ec_encode_data_row_passes(ctx, orc, length, per):
     orc.encode_data(length, k, rows, g, data, ref)
     bad = [r for r in range(rows) if not (d_out[r].cpu().numpy() == ref[r]).all()]
     assert not bad, f"rows {bad} differ"
+
+
+def test_host_io_pipelined_ragged_chunks(ctx):
+    """bench.host_io_pipelined (the overlapped PCIe-inclusive path): 6 blocks
+    in chunks of 4 (a ragged last chunk), survivors shipped as row runs; the
+    recovered rows on the device equal the originals and the host copies
+    equal the device rows."""
+    sys.path.insert(0, os.path.dirname(HERE))
+    import bench
+    r = bench.host_io_pipelined(rsgpu, ctx, 16, 8, 64000, 6, seed=3, chunk=4, reps=1)
+    assert r["verified"] and r["blocks"] == 6
