@@ -125,6 +125,29 @@ def host_io_rate(rsgpu, ctx, k, e, L, blocks, seed, reps=3):
             "verified": ok}
 
 
+def survivor_runs(err, k, pitch, chunk):
+    """Byte ranges (offset, length) of the surviving source rows of every
+    block in a [blocks][k][pitch] row array, merged into runs of consecutive
+    rows and grouped by chunk of `chunk` blocks.  err: [blocks][e] erased
+    source indices (isa_decoder's erasure list)."""
+    import numpy as np
+    blocks = len(err)
+    runs = [[] for _ in range((blocks + chunk - 1) // chunk)]
+    for blk in range(blocks):
+        live = np.ones(k, bool)
+        live[np.asarray(err[blk], dtype=np.int64)] = False
+        j = 0
+        while j < k:
+            if live[j]:
+                j0 = j
+                while j < k and live[j]:
+                    j += 1
+                runs[blk // chunk].append(((blk * k + j0) * pitch, (j - j0) * pitch))
+            else:
+                j += 1
+    return runs
+
+
 def host_io_pipelined(rsgpu, ctx, k, e, L, blocks, seed, chunk=4, reps=3):
     """The host_io_rate workload with the copies overlapped: the blocks go in
     chunks of `chunk` blocks through three streams (H2D, compute, D2H) joined
@@ -146,22 +169,8 @@ def host_io_pipelined(rsgpu, ctx, k, e, L, blocks, seed, chunk=4, reps=3):
     # one decode workspace per chunk: the chunks' decodes may overlap their copies
     wss = [torch.empty(rsgpu.decode_workspace_bytes(k, e, chunk), dtype=torch.uint8,
                        device=enc.src.device) for _ in range(nch)]
-    # decoder side ships only the survivors: per block, the runs of
-    # consecutive non-erased source rows (byte ranges of src), found untimed
-    import numpy as np
-    runs = [[] for _ in range(nch)]
-    for blk in range(blocks):
-        live = np.ones(k, bool)
-        live[dec.err_host[blk]] = False
-        j = 0
-        while j < k:
-            if live[j]:
-                j0 = j
-                while j < k and live[j]:
-                    j += 1
-                runs[blk // chunk].append(((blk * k + j0) * enc.pitch, (j - j0) * enc.pitch))
-            else:
-                j += 1
+    # decoder side ships only the survivors (found untimed)
+    runs = survivor_runs(dec.err_host, k, enc.pitch, chunk)
     s_in, s_cmp, s_out = torch.cuda.Stream(), torch.cuda.Stream(), torch.cuda.Stream()
     prev_stream = torch.cuda.current_stream()
     ctx.set_stream(s_cmp.cuda_stream)

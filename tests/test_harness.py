@@ -56,3 +56,31 @@ DROPIN = os.path.join(ROOT, "storage-benchmarks_amd", "bin", "plugin_dropin_test
 def test_dropin_rejects_bad_config_before_touching_the_gpu():
     r = subprocess.run([DROPIN, "16-64000-8"], capture_output=True, text=True)
     assert r.returncode == 2 and "symbols:symbol_size:erased" in r.stderr
+
+
+@pytest.mark.parametrize("k,e,blocks,chunk", [(16, 8, 6, 4), (64, 32, 9, 2), (5, 4, 3, 4), (10, 0, 2, 1)])
+def test_survivor_runs_cover_exactly_the_live_rows(k, e, blocks, chunk):
+    """bench.survivor_runs (the pipelined host-IO path's decoder-side copies):
+    the runs of each chunk are disjoint, lie inside the chunk's blocks and
+    cover exactly the non-erased source rows."""
+    import sys
+    import numpy as np
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    pitch = 256
+    err = rsgpu.erasure_patterns(7, 0, blocks, k, e) if e else np.zeros((blocks, 0), np.uint8)
+    runs = bench.survivor_runs(err, k, pitch, chunk)
+    assert len(runs) == (blocks + chunk - 1) // chunk
+    for i, rr in enumerate(runs):
+        got = np.zeros(blocks * k, bool)
+        for off, n in rr:
+            assert off % pitch == 0 and n % pitch == 0 and n > 0
+            rows = np.arange(off // pitch, (off + n) // pitch)
+            assert not got[rows].any()
+            got[rows] = True
+        want = np.zeros(blocks * k, bool)
+        for blk in range(i * chunk, min(blocks, (i + 1) * chunk)):
+            live = np.ones(k, bool)
+            live[np.asarray(err[blk], np.int64)] = False
+            want[blk * k:(blk + 1) * k] = live
+        assert (got == want).all()
