@@ -53,6 +53,11 @@ const char *rsgpu_version(void);
  * stream is the device's null stream until rsgpu_set_stream(). */
 int rsgpu_create(int device, rsgpu_ctx **out);
 int rsgpu_destroy(rsgpu_ctx *ctx);
+/* Moves the context to another stream.  Work already enqueued on the old
+ * stream is ordered before anything the context enqueues afterwards (the new
+ * stream waits on an event recorded on the old one): the context's internal
+ * scratch and staging buffers are never reused while an earlier kernel may
+ * still read them. */
 int rsgpu_set_stream(rsgpu_ctx *ctx, void *hip_stream);
 void *rsgpu_get_stream(rsgpu_ctx *ctx);
 int rsgpu_synchronize(rsgpu_ctx *ctx);
@@ -117,17 +122,36 @@ int rsgpu_encode_blocks(rsgpu_ctx *ctx, int k, int e, size_t len, size_t pitch, 
                         const unsigned char *d_src, unsigned char *d_parity,
                         const unsigned char *coef);
 
-/* Device workspace needed by rsgpu_decode_blocks for this geometry. */
+/* Device workspace needed by rsgpu_decode_blocks for this geometry (any
+ * decode kernel choice). */
 size_t rsgpu_decode_workspace_bytes(int k, int e, size_t blocks);
 
+/* Decode kernel of rsgpu_decode_blocks (per context; every choice recovers
+ * the same bytes):
+ *   AUTO        the measured-fastest choice per code (the default)
+ *   ONE_MATRIX  closed-form e x k decode rows V_E^-1 [V_kept | I] (e <= 32),
+ *               one threaded-code pass over the k - e survivors + e parity
+ *   FUSED       syndromes and the e x e solve per column tile in one kernel
+ *               (e <= 32, k <= 128)
+ *   GENERAL     the reference's k x k survivor-matrix inversion on the
+ *               device (isa.cpp:177-204), then the decode rows; any e
+ * A choice that does not apply to a geometry falls back to GENERAL. */
+#define RSGPU_DECODE_AUTO 0
+#define RSGPU_DECODE_ONE_MATRIX 1
+#define RSGPU_DECODE_FUSED 2
+#define RSGPU_DECODE_GENERAL 3
+int rsgpu_set_decode_kernel(rsgpu_ctx *ctx, int kernel);
+
 /* isa_decoder::decode_all over `blocks` blocks (isa.cpp:169-213): for block
- * b the `e` erased ORIGINAL indices d_err[b][0..e-1] (ascending, as the
- * std::set iterates, isa.cpp:150-153) are rebuilt from the surviving
+ * b the `e` erased ORIGINAL indices d_err[b][0..e-1] (strictly ascending, as
+ * the std::set iterates, isa.cpp:150-153) are rebuilt from the surviving
  * originals and all e parity rows.  On the device: survivor matrix ->
  * gf_invert_matrix -> decode rows -> dot product into out[b][i] (symbol
- * d_err[b][i]).  d_status[b] = 0, or -1 for a singular matrix ("BAD MATRIX",
- * isa.cpp:185-190; that block's output is unspecified).  d_workspace holds
- * rsgpu_decode_workspace_bytes() bytes. */
+ * d_err[b][i]).  The erased rows of d_src are never read.  d_status[b] = 0;
+ * -1 for a singular matrix ("BAD MATRIX", isa.cpp:185-190); -2 for a
+ * malformed erasure list (not strictly ascending, or an index >= k).  A
+ * block with a non-zero status is skipped; its output is unspecified.
+ * d_workspace holds rsgpu_decode_workspace_bytes() bytes. */
 int rsgpu_decode_blocks(rsgpu_ctx *ctx, int k, int e, size_t len, size_t pitch, size_t blocks,
                         const unsigned char *d_src, const unsigned char *d_parity,
                         const unsigned char *d_err, unsigned char *d_out, void *d_workspace,
@@ -147,6 +171,26 @@ int rsgpu_decode_prepare(rsgpu_ctx *ctx, int k, int e, size_t len, size_t pitch,
 int rsgpu_decode_apply(rsgpu_ctx *ctx, int k, int e, size_t len, size_t pitch, size_t blocks,
                        const unsigned char *d_src, const unsigned char *d_parity,
                        unsigned char *d_out, void *d_workspace, const int *d_status);
+
+/* General erasure decode: ISA-L's gf_gen_decode_matrix + recovery
+ * (isa-l_open_src_2.13/erasure_code/erasure_code_base_test.c:133-213, :292-
+ * 308) for any m x k encode matrix and erasures among data AND parity rows.
+ *   encode_matrix  HOST m x k row-major (identity on top, as gf_gen_rs_matrix
+ *                  / gf_gen_cauchy1_matrix make it), or NULL for
+ *                  gf_gen_rs_matrix(m, k)
+ *   d_src [blocks][k] rows, d_parity [blocks][m-k] rows (pitch `pitch`)
+ *   d_err [blocks][nerrs] erased row indices in [0, m), strictly ascending
+ *   d_out [blocks][nerrs] recovered rows, in d_err order
+ * Survivors are the first k rows not erased, ascending; when their matrix is
+ * singular the reference's retry (replace the last survivor by a later row,
+ * :163-184) runs, and only when that fails the block gets status -1 ("BAD
+ * MATRIX").  Status -2: malformed list (not ascending, index >= m, or more
+ * than m - k erasures).  Erased rows are never read. */
+size_t rsgpu_decode_general_workspace_bytes(int k, int m, int nerrs, size_t blocks);
+int rsgpu_decode_general(rsgpu_ctx *ctx, int k, int m, size_t len, size_t pitch, size_t blocks,
+                         const unsigned char *encode_matrix, const unsigned char *d_src,
+                         const unsigned char *d_parity, const unsigned char *d_err, int nerrs,
+                         unsigned char *d_out, void *d_workspace, int *d_status);
 
 /* isa_decoder::verify_data (isa.cpp:215-229) on the device: adds to
  * d_mismatch[b] the number of bytes where out[b][i] != src[b][d_err[b][i]]. */

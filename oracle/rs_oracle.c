@@ -365,3 +365,93 @@ void orc_erasure_pattern(uint64_t seed, uint64_t blk, int k, int e, uint8_t *err
         if (in[i])
             err_list[n++] = (uint8_t)i;
 }
+
+/* erasure_code/erasure_code_base_test.c:133-213 gf_gen_decode_matrix:
+ * survivors = the first k rows of the m-row code not listed in err_list
+ * (ascending; decode_index), their k x k matrix inverted; when it is
+ * singular and fewer than m - k rows are erased, the last survivor steps
+ * `incr` rows further (incr cumulative, skipping listed parity rows in
+ * err_list[nsrcerrs .. nerrs - nsrcerrs) as the loop there is bounded) until
+ * an invertible set is found or the rows run out.  Decode rows: row
+ * err_list[i] of the inverse for data erasures, encode row x inverse for
+ * parity erasures.  err_list must be ascending (data erasures first, as
+ * gen_err_list builds it).  Returns 0, or -2 (NO_INVERT_MATRIX, "BAD
+ * MATRIX").  decode_index: k entries, decode_matrix: nerrs x k. */
+int orc_gen_decode_matrix(const uint8_t *encode_matrix, int k, int m, const uint8_t *err_list,
+                          int nerrs, uint8_t *decode_matrix, int *decode_index)
+{
+    orc_init();
+    uint8_t *in_err = calloc((size_t)m + 1, 1);
+    uint8_t *b = malloc((size_t)k * k), *inv = malloc((size_t)k * k);
+    int nsrcerrs = 0, rc = 0;
+    for (int i = 0; i < nerrs; ++i) {
+        in_err[err_list[i]] = 1;
+        nsrcerrs += err_list[i] < k;
+    }
+    for (int i = 0, r = 0; i < k; ++i, ++r) {
+        while (in_err[r])
+            ++r;
+        decode_index[i] = r;
+    }
+    int incr = 0;
+    for (;;) {
+        for (int i = 0; i < k; ++i)
+            memcpy(b + (size_t)k * i, encode_matrix + (size_t)k * decode_index[i], (size_t)k);
+        if (orc_invert_matrix(b, inv, k) == 0)
+            break;
+        if (nerrs == m - k) {
+            rc = -2;
+            break;
+        }
+        ++incr;
+        for (int i = nsrcerrs; i < nerrs - nsrcerrs; ++i)
+            if (err_list[i] == decode_index[k - 1] + incr)
+                ++incr;
+        if (decode_index[k - 1] + incr >= m) {
+            rc = -2;
+            break;
+        }
+        decode_index[k - 1] += incr;
+    }
+    if (rc == 0) {
+        for (int i = 0; i < nsrcerrs; ++i)
+            memcpy(decode_matrix + (size_t)k * i, inv + (size_t)k * err_list[i], (size_t)k);
+        for (int p = nsrcerrs; p < nerrs; ++p)
+            for (int i = 0; i < k; ++i) {
+                uint8_t s = 0;
+                for (int j = 0; j < k; ++j)
+                    s ^= g_mul[inv[j * k + i]][encode_matrix[(size_t)k * err_list[p] + j]];
+                decode_matrix[(size_t)k * p + i] = s;
+            }
+    }
+    free(in_err);
+    free(b);
+    free(inv);
+    return rc;
+}
+
+/* The recovery of erasure_code_base_test.c:299-308: recov[i] =
+ * buffs[decode_index[i]], then ec_init_tables + ec_encode_data_base with
+ * the decode matrix.  rows: m row pointers (data 0..k-1, parity k..m-1);
+ * out: nerrs rows.  Returns gen_decode_matrix's status. */
+int orc_decode_general(const uint8_t *encode_matrix, int k, int m, int len,
+                       const uint8_t *err_list, int nerrs, uint8_t *const *rows,
+                       uint8_t *const *out)
+{
+    uint8_t *dm = malloc((size_t)k * (nerrs ? nerrs : 1));
+    uint8_t *g = malloc((size_t)32 * k * (nerrs ? nerrs : 1));
+    int *idx = malloc(sizeof(int) * (size_t)k);
+    uint8_t **recov = malloc(sizeof(uint8_t *) * (size_t)k);
+    int rc = orc_gen_decode_matrix(encode_matrix, k, m, err_list, nerrs, dm, idx);
+    if (rc == 0 && nerrs > 0) {
+        for (int i = 0; i < k; ++i)
+            recov[i] = rows[idx[i]];
+        orc_init_tables(k, nerrs, dm, g);
+        orc_encode_data(len, k, nerrs, g, recov, out);
+    }
+    free(dm);
+    free(g);
+    free(idx);
+    free(recov);
+    return rc;
+}

@@ -24,6 +24,11 @@ void orc_encode_block(int k, int e, int len, uint8_t *const *data, uint8_t *cons
 int orc_decode_block(int k, int e, int len, const uint8_t *err_list,
                      uint8_t *const *data, uint8_t *const *parity, uint8_t *const *out);
 int orc_decode_matrix(int k, int e, const uint8_t *err_list, uint8_t *c_out);
+int orc_gen_decode_matrix(const uint8_t *encode_matrix, int k, int m, const uint8_t *err_list,
+                          int nerrs, uint8_t *decode_matrix, int *decode_index);
+int orc_decode_general(const uint8_t *encode_matrix, int k, int m, int len,
+                       const uint8_t *err_list, int nerrs, uint8_t *const *rows,
+                       uint8_t *const *out);
 uint64_t orc_synth_word(uint64_t seed, uint64_t row, uint64_t word);
 void orc_synth_row(uint64_t seed, uint64_t row, uint8_t *dst, size_t len);
 void orc_erasure_pattern(uint64_t seed, uint64_t blk, int k, int e, uint8_t *err_list);

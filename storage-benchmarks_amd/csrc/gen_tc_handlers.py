@@ -17,8 +17,7 @@ v0..v63 with amdgpu_num_vgpr(64), so v64..v127 belong to the asm alone):
     address banks       s[64:79], s[84:99]; m0 save s63; chain continuation s[80:81]; planes v[24:31]
     (all of these are clobbers of the one asm statement per chunk)
 
-usage: gen_tc_handlers.py OUT.inc [SYN.inc]
-  SYN.inc: compile-time syndrome blocks of the fused decode (rs_decode_fused.hip)
+usage: gen_tc_handlers.py OUT.inc
 """
 import os
 import sys
@@ -177,59 +176,22 @@ def chunk(nt: int) -> list:
             ins += sload(t + 1, nxt) + ([] if late else stage(t + 1))
         ins += tables()
         # index mode on once per source; slots switch the index only
-        if os.environ.get("RSGPU_TC_FAKE") == "inline":  # timing experiment only: wrong products
-            for slot in range(8):
-                ins += mac_lines(0x53 + 16 * slot, slot)
-        else:
-            mode = False
-            for s0, ks, ix in GROUPS:
-                if ix and not mode:
-                    ins.append(f"s_set_gpr_idx_on {ix}, gpr_idx(SRC0,DST)")
-                    mode = True
-                elif ix:
-                    ins.append(f"s_set_gpr_idx_idx {ix}")
-                for i in range(1, len(ks)):  # continuations of the chain
-                    ra, sl = RA_LIST[ks[i - 1]], s0 + i
-                    ins.append(f"s_mov_b64 s[{ra}:{ra + 1}], s[{cur + 2 * sl}:{cur + 2 * sl + 1}]")
-                ins.append(f"s_swappc_b64 s[{RET}:{RET + 1}], s[{cur + 2 * s0}:{cur + 2 * s0 + 1}]")
-            if mode:
-                ins.append("s_set_gpr_idx_off")
+        mode = False
+        for s0, ks, ix in GROUPS:
+            if ix and not mode:
+                ins.append(f"s_set_gpr_idx_on {ix}, gpr_idx(SRC0,DST)")
+                mode = True
+            elif ix:
+                ins.append(f"s_set_gpr_idx_idx {ix}")
+            for i in range(1, len(ks)):  # continuations of the chain
+                ra, sl = RA_LIST[ks[i - 1]], s0 + i
+                ins.append(f"s_mov_b64 s[{ra}:{ra + 1}], s[{cur + 2 * sl}:{cur + 2 * sl + 1}]")
+            ins.append(f"s_swappc_b64 s[{RET}:{RET + 1}], s[{cur + 2 * s0}:{cur + 2 * s0 + 1}]")
+        if mode:
+            ins.append("s_set_gpr_idx_off")
         if late and t + 1 < nt:  # the planes are free once the dispatch is done
             ins += stage(t + 1)
     ins += [f"s_mov_b32 m0, s{SM0}", "s_nop 0"]
-    return ins
-
-
-def gf_pow2(n: int) -> int:
-    v = 1
-    for _ in range(n % 255):
-        v = gf_mul(v, 2)
-    return v
-
-
-# Codes with a fused syndrome decode (rs_decode_fused.hip): (K, E, C) =
-# (sources, parity rows, Horner chunk) of the gf_gen_rs_matrix code; E <= 32.
-# C = 8 keeps the fused kernel's code (every wave group's blocks + the 256
-# handlers) inside the instruction cache: C = 16 at (64, 32) thrashed it.
-# C = 16 at (64, 32) measured 32.5-32.6 ms against 32.3-32.4 for C = 8 even
-# with shared scaffolding (half the twiddles do not pay for the larger code).
-SYN_PLANS = [(16, 4, 8), (16, 8, 8), (64, 32, 8), (64, 16, 8), (100, 20, 8), (5, 4, 5),
-             (20, 7, 8)]
-
-
-def mac_lines(c: int, slot: int) -> list:
-    """acc slot `slot` ^= c * (current source) from the L/H tables."""
-    ins = []
-    for b in range(8):
-        m = mat_row(c, b)
-        lo, hi = m & 15, m >> 4
-        acc = ACC + 8 * slot + b
-        if lo and hi:
-            ins.append(f"v_bitop3_b32 v{acc}, v{acc}, v{reg_l(lo)}, v{reg_h(hi)} bitop3:0x96")
-        elif lo:
-            ins.append(f"v_xor_b32_e32 v{acc}, v{reg_l(lo)}, v{acc}")
-        elif hi:
-            ins.append(f"v_xor_b32_e32 v{acc}, v{reg_h(hi)}, v{acc}")
     return ins
 
 
@@ -244,129 +206,8 @@ def tables() -> list:
     return ins
 
 
-def syn_block(K: int, E: int, g: int, t: int) -> list:
-    """Compile-time syndrome MAC: source at chunk position t into the slots of
-    wave group g (rows r = 8g + s < E), coefficient 2^(r t)."""
-    ins = tables()
-    for s in range(8):
-        r = 8 * g + s
-        if r < E:
-            ins += mac_lines(gf_pow2(r * t), s)
-    return ins
-
-
-def lin_inplace(c: int, slot: int) -> list:
-    """acc slot `slot` := c * acc (the 8x8 GF(2) matrix of c applied to the
-    planes in place).  Outputs are written straight into their own plane when
-    no later output still needs that plane's old value; otherwise the old
-    value is first saved in a temp (v32..v39).  Identity rows cost nothing."""
-    base = ACC + 8 * slot
-    need = {b: [a for a in range(8) if (mat_row(c, b) >> a) & 1] for b in range(8)}
-    todo = [b for b in range(8) if need[b] != [b]]
-    loc = {a: base + a for a in range(8)}
-    ins, tmp = [], 32
-
-    def xor_into(dst, srcs):
-        if dst in srcs:  # the old value of dst must be read by the first op
-            srcs = [dst] + [x for x in srcs if x != dst]
-        if len(srcs) == 1:
-            ins.append(f"v_mov_b32_e32 v{dst}, v{srcs[0]}")
-            return
-        if len(srcs) == 2:
-            ins.append(f"v_xor_b32_e32 v{dst}, v{srcs[0]}, v{srcs[1]}")
-            return
-        ins.append(f"v_bitop3_b32 v{dst}, v{srcs[0]}, v{srcs[1]}, v{srcs[2]} bitop3:0x96")
-        rest = srcs[3:]
-        while len(rest) >= 2:
-            ins.append(f"v_bitop3_b32 v{dst}, v{dst}, v{rest[0]}, v{rest[1]} bitop3:0x96")
-            rest = rest[2:]
-        if rest:
-            ins.append(f"v_xor_b32_e32 v{dst}, v{dst}, v{rest[0]}")
-
-    while todo:
-        free = [b for b in todo if all(b not in need[o] for o in todo if o != b)]
-        b = free[0] if free else todo[0]
-        if not free:  # every remaining output still needs in_b: keep a copy
-            ins.append(f"v_mov_b32_e32 v{tmp}, v{base + b}")
-            loc[b] = tmp
-            tmp += 1
-            assert tmp <= 40
-        xor_into(base + b, [loc[a] for a in need[b]])
-        todo.remove(b)
-    return ins
-
-
-def syn_twiddle(E: int, C: int, g: int) -> list:
-    """Horner step between chunks: slot s (row r) *= 2^(C r)."""
-    ins = []
-    for s in range(8):
-        r = 8 * g + s
-        if r < E:
-            ins += lin_inplace(gf_pow2(C * r), s)
-    return ins
-
-
-def syn_prescale(K: int, E: int, C: int, g: int) -> list:
-    """Parity rows enter the accumulators before the first chunk, scaled by
-    2^(-C r (NCH-1)): the NCH-1 Horner twiddles bring them back to P_r."""
-    nch = (K + C - 1) // C
-    ins = []
-    for s in range(8):
-        r = 8 * g + s
-        if r < E:
-            ins += lin_inplace(gf_pow2((-C * r * (nch - 1)) % 255), s)
-    return ins
-
-
-def write_syn(path: str) -> None:
-    """C++ specializations SynBlock<K,E,G,T> / SynTwiddle<K,E,G> / XorSlot<S>
-    wrapping the generated asm (rs_decode_fused.hip declares the primaries)."""
-    out = ["// generated by gen_tc_handlers.py -- do not edit"]
-    tab = [r for r in TABLE_REGS if r not in PLANE_REG]
-    clob = ", ".join([f'"v{r}"' for r in tab] + [f'"v{ACC + i}"' for i in range(64)])
-    plane_ops = ", ".join(f'"{{v{r}}}"(P[{a}])' for a, r in enumerate(PLANE_REG))
-    tw_clob = ", ".join([f'"v{r}"' for r in range(32, 40)] + [f'"v{ACC + i}"' for i in range(64)])
-
-    def asm_text(ins):
-        return " ".join(f'"{i}\\n"' for i in ins)
-
-    # MAC blocks depend on (K, E, g, t) only: one set per code, t < the
-    # largest chunk any plan of that code uses; twiddles depend on C too
-    tmax = {}
-    for K, E, C in SYN_PLANS:
-        tmax[(K, E)] = max(tmax.get((K, E), 0), C)
-    for (K, E), CM in tmax.items():
-        for g in range((E + 7) // 8):
-            for t in range(CM):
-                out.append(f"template <> struct SynBlock<{K}, {E}, {g}, {t}> {{")
-                out.append("    __device__ __forceinline__ static void run(const uint32_t (&P)[8])")
-                out.append(f"    {{ asm volatile({asm_text(syn_block(K, E, g, t))} :: {plane_ops} : {clob}); }}")
-                out.append("};")
-    for K, E, C in SYN_PLANS:
-        for g in range((E + 7) // 8):
-            for name, body in (("SynTwiddle", syn_twiddle(E, C, g)),
-                               ("SynPreScale", syn_prescale(K, E, C, g))):
-                out.append(f"template <> struct {name}<{K}, {E}, {C}, {g}> {{")
-                out.append("    __device__ __forceinline__ static void run()")
-                text = asm_text(body) if body else '""'
-                out.append(f"    {{ asm volatile({text} ::: {tw_clob}); }}")
-                out.append("};")
-    for s in range(8):
-        ins = [f"v_xor_b32_e32 v{ACC + 8 * s + b}, %{b}, v{ACC + 8 * s + b}" for b in range(8)]
-        ops = ", ".join(f'"v"(W[{b}])' for b in range(8))
-        acc_clob = ", ".join(f'"v{ACC + 8 * s + b}"' for b in range(8))
-        out.append(f"template <> struct XorSlot<{s}> {{")
-        out.append("    __device__ __forceinline__ static void run(const uint32_t (&W)[8])")
-        out.append(f"    {{ asm volatile({asm_text(ins)} :: {ops} : {acc_clob}); }}")
-        out.append("};")
-    with open(path, "w") as f:
-        f.write("\n".join(out) + "\n")
-
-
 def main() -> None:
     out = sys.argv[1]
-    if len(sys.argv) > 2:
-        write_syn(sys.argv[2])
     lines = [
         "// generated by gen_tc_handlers.py -- do not edit",
         f"#define RSGPU_TC_STRIDE {STRIDE}",

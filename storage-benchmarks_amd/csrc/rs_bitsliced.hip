@@ -1,4 +1,4 @@
-// rs_bitsliced.hip -- bit-sliced RS(K, E) parity / syndrome kernel with
+// rs_bitsliced.hip -- bit-sliced RS(K, E) parity kernel with
 // compile-time coefficients (the gf_gen_rs_matrix code, isa/ec_base.c:62-79).
 //
 // Why bit-slicing: on gfx950 a wave64 v_bitop3/v_xor/v_and issues in ~2
@@ -30,9 +30,6 @@
 // the lane's 8 dwords (12 block swaps), and the same routine converts the
 // accumulators back to bytes.
 //
-// SYN (decode): sources whose bit is set in the block's erasure mask are
-// skipped and the finished sums are XORed with the parity rows, giving the
-// syndromes s_p = P_p ^ sum_{j not erased} 2^(p j) d_j.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -126,10 +123,8 @@ __device__ __forceinline__ void consume(uint32_t (&acc)[NR][8], const uint32_t (
 
 struct Args {
     const uint8_t* src;   // [B][K] rows
-    const uint8_t* par;   // [B][E] parity rows (SYN only)
     uint8_t* out;         // [B][E] rows
     long long pitch, len;
-    const uint64_t* emask;  // [B][2] erasure bitmask of the K originals (SYN only)
 };
 
 // LDS part: S sources of [2 halves][64 lanes] x 16 B; two parts double-buffer
@@ -137,36 +132,17 @@ struct Args {
 // consecutive parts.
 constexpr int S = 8;
 
-// 64-bit wave-uniform copy (readfirstlane returns int: widen through
-// uint32_t, never sign-extend the low word)
-__device__ __forceinline__ uint64_t uniform64(uint64_t x)
-{
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)x);
-    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(x >> 32));
-    return ((uint64_t)hi << 32) | lo;
-}
-
-template <int K, bool SYN>
-__device__ __forceinline__ bool is_live(int j, uint64_t em0, uint64_t em1)
-{
-    if (j >= K)
-        return false;
-    if constexpr (SYN)
-        return !(((j < 64 ? em0 >> j : em1 >> (j - 64)) & 1));
-    return true;
-}
-
 // Sources T = PART*S + t (t < S, T < C) of the current chunk from the LDS part.
-template <class P, int K, int C, int R0, int NR, int PART, bool SYN>
+template <class P, int K, int C, int R0, int NR, int PART>
 __device__ __forceinline__ void consume_part(uint32_t (&acc)[NR][8], const uint4* buf, int lane,
-                                             int j0, uint64_t em0, uint64_t em1)
+                                             int j0)
 {
     [&]<int... Ts>(std::integer_sequence<int, Ts...>) {
         (
             [&] {
                 constexpr int T = PART * S + Ts;
                 if constexpr (T < C) {
-                    if (is_live<K, SYN>(j0 + Ts, em0, em1)) {
+                    if (j0 + Ts < K) {
                         const uint4 u = buf[(Ts * 2 + 0) * 64 + lane];
                         const uint4 v = buf[(Ts * 2 + 1) * 64 + lane];
                         const uint32_t pl[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
@@ -185,7 +161,7 @@ __device__ __forceinline__ void consume_part(uint32_t (&acc)[NR][8], const uint4
 // chunk by chunk (Horner order, last chunk first) through the LDS parts:
 // while part n is transposed in place and consumed, part n+1 is already in
 // flight by LDS-DMA (global_load_lds_dwordx4, counted vmcnt, raw barriers).
-template <int K, int E, int C, int NW, bool SYN, int G>
+template <int K, int E, int C, int NW, int G>
 __device__ __forceinline__ void run_group(const Args& a, uint4 (*lds)[S * 2 * 64])
 {
     using P = PlanHolder<K, E, C>;
@@ -202,12 +178,7 @@ __device__ __forceinline__ void run_group(const Args& a, uint4 (*lds)[S * 2 * 64
     const bool inb = off + 32 <= a.len;
     const long long loff = inb ? off : 0;  // out-of-range lanes re-read the row head
     const uint8_t* sb = a.src + (size_t)b * K * a.pitch;
-    uint64_t em0 = 0, em1 = 0;
-    if constexpr (SYN) {  // wave-uniform: keep the masks (and every test of them) scalar
-        em0 = uniform64(a.emask[2 * b]);
-        em1 = uniform64(a.emask[2 * b + 1]);
-    }
-    auto live = [&](int j) { return is_live<K, SYN>(j, em0, em1); };
+    auto live = [&](int j) { return j < K; };
     const uint32_t m4 = vconst(0x0F0F0F0Fu), m2 = vconst(0x33333333u), m1 = vconst(0x55555555u);
     const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint4*)&lds[0][0];
 
@@ -218,7 +189,7 @@ __device__ __forceinline__ void run_group(const Args& a, uint4 (*lds)[S * 2 * 64
         const int p = n % NP;
         return min(S, C - p * S);
     };
-    // this wave's share of step n: t = G, G + NW, ... (live sources only)
+    // this wave's share of step n: t = G, G + NW, ...
     auto issue = [&](int n) {
         const int j0 = first_src(n), nt = part_len(n);
         const uint32_t base = lds0 + (uint32_t)((n & 1) * S * 2 * 64 * 16);
@@ -267,7 +238,7 @@ __device__ __forceinline__ void run_group(const Args& a, uint4 (*lds)[S * 2 * 64
             twiddle_rows<P, R0, NR>(acc, std::make_integer_sequence<int, NR>{});
         // consume part `part` of the chunk: compile-time T = part*S + t
         [&]<int... Ps>(std::integer_sequence<int, Ps...>) {
-            ((part == Ps ? consume_part<P, K, C, R0, NR, Ps, SYN>(acc, buf, lane, j0, em0, em1)
+            ((part == Ps ? consume_part<P, K, C, R0, NR, Ps>(acc, buf, lane, j0)
                          : void()),
              ...);
         }(std::make_integer_sequence<int, NP>{});
@@ -284,13 +255,6 @@ __device__ __forceinline__ void run_group(const Args& a, uint4 (*lds)[S * 2 * 64
         for (int q = 0; q < 8; ++q)
             W[q] = acc[r][q];
         tr8(W, m4, m2, m1);
-        if constexpr (SYN) {
-            uint32_t Pp[8];
-            load32(a.par + ((size_t)b * E + R0 + r) * a.pitch, off, true, Pp);
-#pragma unroll
-            for (int q = 0; q < 8; ++q)
-                W[q] ^= Pp[q];
-        }
         store32(ob + (size_t)(R0 + r) * a.pitch, off, W);
     }
 }
@@ -305,26 +269,23 @@ constexpr int bs_waves_per_simd()
     return (E + NW - 1) / NW > 8 ? 2 : 16 / NW;
 }
 
-template <int K, int E, int C, int NW, bool SYN>
+template <int K, int E, int C, int NW>
 __global__ __launch_bounds__(64 * NW, (bs_waves_per_simd<E, NW>())) void k_rs_bs(Args a)
 {
     __shared__ uint4 lds[2][S * 2 * 64];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     [&]<int... Gs>(std::integer_sequence<int, Gs...>) {
-        ((wave == Gs ? run_group<K, E, C, NW, SYN, Gs>(a, lds) : void()), ...);
+        ((wave == Gs ? run_group<K, E, C, NW, Gs>(a, lds) : void()), ...);
     }(std::make_integer_sequence<int, NW>{});
 }
 
 template <int K, int E, int C, int NW>
-hipError_t launch(const uint8_t* src, const uint8_t* par, uint8_t* out, long long pitch,
-                  long long len, long long blocks, const uint64_t* emask, hipStream_t st)
+hipError_t launch(const uint8_t* src, uint8_t* out, long long pitch, long long len,
+                  long long blocks, hipStream_t st)
 {
-    Args a{src, par, out, pitch, len, emask};
+    Args a{src, out, pitch, len};
     dim3 grid((unsigned)((len + 2047) / 2048), (unsigned)blocks);
-    if (emask)
-        hipLaunchKernelGGL((k_rs_bs<K, E, C, NW, true>), grid, dim3(64 * NW), 0, st, a);
-    else
-        hipLaunchKernelGGL((k_rs_bs<K, E, C, NW, false>), grid, dim3(64 * NW), 0, st, a);
+    hipLaunchKernelGGL((k_rs_bs<K, E, C, NW>), grid, dim3(64 * NW), 0, st, a);
     return hipGetLastError();
 }
 
@@ -337,17 +298,16 @@ bool rs_bitsliced_available(int k, int e)
            (k == 64 && e == 16);
 }
 
-hipError_t launch_rs_bitsliced(int k, int e, const uint8_t* src, const uint8_t* par, uint8_t* out,
-                               long long pitch, long long len, long long blocks,
-                               const uint64_t* emask, hipStream_t st)
+hipError_t launch_rs_bitsliced(int k, int e, const uint8_t* src, uint8_t* out, long long pitch,
+                               long long len, long long blocks, hipStream_t st)
 {
-    if (k == 16 && e == 4) return bs::launch<16, 4, 16, 1>(src, par, out, pitch, len, blocks, emask, st);
-    if (k == 16 && e == 8) return bs::launch<16, 8, 16, 1>(src, par, out, pitch, len, blocks, emask, st);
-    if (k == 64 && e == 32) return bs::launch<64, 32, 16, 4>(src, par, out, pitch, len, blocks, emask, st);
-    if (k == 64 && e == 16) return bs::launch<64, 16, 16, 2>(src, par, out, pitch, len, blocks, emask, st);
-    if (k == 100 && e == 20) return bs::launch<100, 20, 20, 4>(src, par, out, pitch, len, blocks, emask, st);
-    if (k == 5 && e == 4) return bs::launch<5, 4, 5, 1>(src, par, out, pitch, len, blocks, emask, st);
-    if (k == 20 && e == 7) return bs::launch<20, 7, 20, 1>(src, par, out, pitch, len, blocks, emask, st);
+    if (k == 16 && e == 4) return bs::launch<16, 4, 16, 1>(src, out, pitch, len, blocks, st);
+    if (k == 16 && e == 8) return bs::launch<16, 8, 16, 1>(src, out, pitch, len, blocks, st);
+    if (k == 64 && e == 32) return bs::launch<64, 32, 16, 4>(src, out, pitch, len, blocks, st);
+    if (k == 64 && e == 16) return bs::launch<64, 16, 16, 2>(src, out, pitch, len, blocks, st);
+    if (k == 100 && e == 20) return bs::launch<100, 20, 20, 4>(src, out, pitch, len, blocks, st);
+    if (k == 5 && e == 4) return bs::launch<5, 4, 5, 1>(src, out, pitch, len, blocks, st);
+    if (k == 20 && e == 7) return bs::launch<20, 7, 20, 1>(src, out, pitch, len, blocks, st);
     return hipErrorInvalidValue;
 }
 

@@ -4,37 +4,31 @@
 // plus the parked syndromes of the waves beyond the LDS hand-off.
 //
 // Status: the default decode is the one-matrix k_rs_tc (rsgpu_capi.cpp
-// decode_mode); this kernel is the default for (k 100, e 20), where it
-// measured 3 % faster, and RSGPU_DECODE=fused selects it elsewhere.  Its
-// phase 1 runs on threaded code by default (TC1 below); the compile-time
-// Horner form described next is kept behind RSGPU_FUSED_SYN=horner.
+// decode_kernel); this kernel is the default for (k 100, e 20), where it
+// measured 3 % faster, and RSGPU_DECODE_FUSED (rsgpu_set_decode_kernel)
+// selects it for any k <= 128, e <= 32.
 //
-// The two-kernel decode (k_rs_bs<SYN> writes the e syndrome rows to HBM,
-// k_rs_tc reads them back and overwrites them with the data) moves 2 e L
-// more bytes.  Here one workgroup does both for its 2 KB column tile:
+// The two-kernel decode (syndrome rows to HBM, then the solve reading them
+// back) moves 2 e L more bytes.  Here one workgroup does both for its 2 KB
+// column tile, both phases on threaded code (rs_tc.hip's chunk asm):
 //
-//   phase 1  s = P ^ V_kept d_kept        compile-time coefficients 2^(r j)
-//            (the k_rs_bs syndrome: sources streamed by LDS-DMA, bit-
-//            transposed in LDS, Horner over chunks of C sources).  The
-//            parity rows are loaded into the accumulators first, scaled by
-//            2^(-C r (NCH-1)) so the Horner twiddles return them to P_r: their
-//            load overlaps the first LDS-DMA part instead of ending the phase.
-//            The e syndrome rows are stored to this tile of the output rows in
-//            bit-plane form (they stay L2/MALL resident)
-//   phase 2  x = V_E^-1 s                 runtime coefficients, threaded code
-//            (k_rs_tc's chunk asm over the e syndrome rows read back by
-//            LDS-DMA -- already planes, so no input transposes), then the
+//   phase 1  s = P ^ V_kept d_kept        coefficients 2^(r j) of the k - e
+//            surviving originals j (handler addresses from the prepare
+//            kernel), sources streamed by LDS-DMA and bit-transposed in LDS;
+//            the parity rows enter the accumulators first.  Wave G's e/NW
+//            syndrome rows are phase 2's chunk G: waves 0 and 1 hand theirs
+//            over in LDS, later waves park theirs in this tile of the output
+//            rows (L2 / MALL resident) in bit-plane form
+//   phase 2  x = V_E^-1 s                 runtime e x e coefficients over the
+//            syndrome rows (already planes: no input transposes), then the
 //            rows are transposed to bytes and overwrite the syndromes.
 //
 // Both phases keep the accumulators in asm-owned v64..v127 (the compiler is
-// capped at v0..v63, amdgpu_num_vgpr(64)): phase 1's compile-time MAC blocks
-// are generated asm too (gen_tc_handlers.py -> build/syn_blocks.inc).
-// Wave w owns rows 8w..8w+7; NW = ceil(e / 8) waves per workgroup.
+// capped at v0..v63, amdgpu_num_vgpr(64)).  Wave w owns rows 8w..8w+7; NW =
+// ceil(e / 8) waves per workgroup.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include <cstdlib>
-#include <cstring>
 #include <utility>
 
 #include "bitslice.h"
@@ -43,16 +37,6 @@
 
 namespace rsgpu {
 namespace fused {
-
-template <int K, int E, int G, int T>
-struct SynBlock;
-template <int K, int E, int C, int G>
-struct SynTwiddle;
-template <int K, int E, int C, int G>
-struct SynPreScale;
-template <int S>
-struct XorSlot;
-#include "syn_blocks.inc"
 
 using bs::barrier_lds;
 using bs::glds32;
@@ -97,6 +81,7 @@ struct Args {
     const uint8_t* src;                // [B][K] rows
     const uint8_t* par;                // [B][E] rows
     uint8_t* out;                      // [B][E] rows (syndromes, then the data)
+    int K, E;
     long long pitch, len;
     const uint64_t* emask;             // [B][2] erased originals
     const unsigned long long* addr;    // [B][E][8 NW] handler addresses of V_E^-1
@@ -164,55 +149,6 @@ __device__ __forceinline__ void load_slot(const uint8_t* row)
 #undef RSGPU_LD
 }
 
-// SynBlock<K, E, g, T> for the runtime (wave-uniform) wave group g
-template <int K, int E, int T, int NW>
-__device__ __forceinline__ void syn_block(int g, const uint32_t (&P)[8])
-{
-    [&]<int... Gs>(std::integer_sequence<int, Gs...>) {
-        ((g == Gs ? SynBlock<K, E, Gs, T>::run(P) : void()), ...);
-    }(std::make_integer_sequence<int, NW>{});
-}
-
-template <int K, int E, int C, int NW>
-__device__ __forceinline__ void syn_twiddle(int g)
-{
-    [&]<int... Gs>(std::integer_sequence<int, Gs...>) {
-        ((g == Gs ? SynTwiddle<K, E, C, Gs>::run() : void()), ...);
-    }(std::make_integer_sequence<int, NW>{});
-}
-
-template <int K, int E, int C, int NW>
-__device__ __forceinline__ void syn_prescale(int g)
-{
-    [&]<int... Gs>(std::integer_sequence<int, Gs...>) {
-        ((g == Gs ? SynPreScale<K, E, C, Gs>::run() : void()), ...);
-    }(std::make_integer_sequence<int, NW>{});
-}
-
-template <int K, int C, int E, int NW, int PART>
-__device__ __forceinline__ void syn_part(int G, const uint4* buf, int lane, int j0, uint64_t em0,
-                                         uint64_t em1)
-{
-    [&]<int... Ts>(std::integer_sequence<int, Ts...>) {
-        (
-            [&] {
-                constexpr int T = PART * S + Ts;
-                if constexpr (T < C) {
-                    const int j = j0 + Ts;
-                    const bool live = j < K && !(((j < 64 ? em0 >> j : em1 >> (j - 64)) & 1));
-                    if (live) {
-                        const uint4 u = buf[(Ts * 2 + 0) * 64 + lane];
-                        const uint4 v = buf[(Ts * 2 + 1) * 64 + lane];
-                        const uint32_t P[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
-                        syn_block<K, E, T, NW>(G, P);
-                    }
-                    __builtin_amdgcn_sched_barrier(0);
-                }
-            }(),
-            ...);
-    }(std::make_integer_sequence<int, S>{});
-}
-
 // One LDS part of nt sources through the threaded-code chunk asm
 // (gen_tc_handlers.py): la = part base + 16 lane, pa = this wave's handler
 // addresses of the part's first source (NW * 8 per source).
@@ -239,16 +175,12 @@ __device__ __forceinline__ void tc_chunk(uint32_t la, const unsigned long long* 
 #undef RSGPU_TC_RUN
 }
 
-// The scaffolding is shared by every wave group (G runtime, wave-uniform):
-// only the generated MAC / twiddle blocks differ per group, which keeps the
-// executed code of all groups plus the 256 handlers inside the I-cache.
-template <int K, int E, int C, int NW, bool TC1>
+// One wave group G (runtime, wave-uniform) of NW: rows 8G..8G+7.
+template <int NW>
 __device__ __forceinline__ void run_group(const Args& a, uint4 (*lds)[S * 2 * 64], uint8_t* items,
                                           int G)
 {
-    constexpr int NCH = (K + C - 1) / C;
-    constexpr int NP = (C + S - 1) / S;
-    constexpr int NSTEP = NCH * NP;
+    const int K = a.K, E = a.E;
     const int lane = threadIdx.x & 63;
     const int b = blockIdx.y;
     const long long off = (long long)blockIdx.x * 2048 + lane * 32;
@@ -262,156 +194,57 @@ __device__ __forceinline__ void run_group(const Args& a, uint4 (*lds)[S * 2 * 64
     const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint4*)&lds[0][0];
 
     // ---------------- phase 1: syndromes ----------------
+    // The K-E survivors in ascending order, S per LDS part, each wave moving
+    // and transposing slots t = G, G+NW, ...; coefficient 2^(r j) of
+    // survivor j for syndrome row r comes as a handler address from the
+    // prepare kernel's table.  The parity rows enter the accumulators
+    // unscaled.
     FP_DECL
-    if constexpr (TC1) {
-        // Threaded code (the phase-2 machinery): the K-E survivors in
-        // ascending order, S per LDS part, each wave moving and transposing
-        // slots t = G, G+NW, ...; coefficient 2^(r j) of survivor j for
-        // syndrome row r comes as a handler address from the prepare
-        // kernel's table.  No Horner chunks, so no twiddles and the parity
-        // rows enter the accumulators unscaled.
-        constexpr int NL = K - E;
-        constexpr int NSTEP = (NL + S - 1) / S;
-        static_assert(K <= 128, "survivor list: one byte per survivor, two lanes' words");
-        uint32_t vi0 = 0, vi1 = 0;  // lane q: survivor q (q < 64) / 64 + q
-        {
-            auto range = [](int lo, int hi) -> uint64_t {  // bits [lo, hi) of one word
-                lo = max(lo, 0);
-                hi = min(hi, 64);
-                if (hi <= lo)
-                    return 0;
-                const uint64_t below_hi = hi >= 64 ? ~0ull : ((1ull << hi) - 1);
-                return below_hi & ~((1ull << lo) - 1);
-            };
-            const uint64_t lv0 = ~em0 & range(0, K), lv1 = ~em1 & range(0, K - 64);
-            for (int j = lane; j < K; j += 64)
-                if (live(j))
-                    items[__popcll(lv0 & range(0, j)) + __popcll(lv1 & range(-64, j - 64))] = (uint8_t)j;
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // own lanes' writes, in order
-            vi0 = lane < NL ? items[lane] : 0;
-            if constexpr (NL > 64)
-                vi1 = 64 + lane < NL ? items[64 + lane] : 0;
-        }
-        auto survivor = [&](int q) -> int {
-            if constexpr (NL > 64)
-                return __builtin_amdgcn_readlane((int)(q < 64 ? vi0 : vi1), q & 63);
-            return __builtin_amdgcn_readlane((int)vi0, q);
+    const int NL = K - E;
+    const int NSTEP = (NL + S - 1) / S;
+    uint32_t vi0 = 0, vi1 = 0;  // lane q: survivor q (q < 64) / 64 + q
+    {
+        auto range = [](int lo, int hi) -> uint64_t {  // bits [lo, hi) of one word
+            lo = max(lo, 0);
+            hi = min(hi, 64);
+            if (hi <= lo)
+                return 0;
+            const uint64_t below_hi = hi >= 64 ? ~0ull : ((1ull << hi) - 1);
+            return below_hi & ~((1ull << lo) - 1);
         };
-        auto part_n = [&](int n) { return min(S, NL - n * S); };
-        auto issue1 = [&](int n) {
-            const uint32_t base = lds0 + (uint32_t)((n & 1) * S * 2 * 64 * 16);
-            for (int t = G; t < part_n(n); t += NW)
-                glds32(sb + (size_t)survivor(n * S + t) * a.pitch, (uint32_t)loff,
-                       base + (uint32_t)(t * 2 * 64 * 16));
-        };
-        auto own1 = [&](int n) {
-            const int nt = part_n(n);
-            return nt > G ? 2 * ((nt - G + NW - 1) / NW) : 0;
-        };
-        asm volatile(RSGPU_TC_ZERO ::: RSGPU_TC_ACC_CLOBBERS);
-        // parity rows straight into this wave's accumulators (unscaled)
-        [&]<int... Ss>(std::integer_sequence<int, Ss...>) {
-            ((G * 8 + Ss < E ? load_slot<Ss>(a.par + ((size_t)b * E + G * 8 + Ss) * a.pitch + loff)
-                             : void()),
-             ...);
-        }(std::make_integer_sequence<int, 8>{});
-        issue1(0);
-        if (NSTEP > 1)
-            issue1(1);
-        wait_vm(own1(0) + (NSTEP > 1 ? own1(1) : 0));  // the (older) parity loads have landed
-        [&]<int... Ss>(std::integer_sequence<int, Ss...>) {
-            (
-                [&] {
-                    if (G * 8 + Ss < E) {
-                        uint32_t W[8];
-                        read_slot<Ss>(W);
-                        tr8(W, m4, m2, m1);
-                        write_slot<Ss>(W);
-                    }
-                }(),
-                ...);
-        }(std::make_integer_sequence<int, 8>{});
-        FP_MARK(12);
-        const unsigned long long* sp = a.syn_addr + (size_t)b * NL * (NW * 8) + G * 8;
-        for (int n = 0; n < NSTEP; ++n) {
-            const int nt = part_n(n);
-            FP_MARK(5);
-            if (n == 0) {
-                FP_MARK(0);
-                wait_vm(NSTEP > 1 ? own1(1) : 0);
-            } else if (n + 1 < NSTEP) {
-                issue1(n + 1);
-                FP_MARK(0);
-                wait_vm(own1(n + 1));
-            } else {
-                wait_vm(0);
-            }
-            FP_MARK(1);
-            uint4* buf = lds[n & 1];
-            for (int t = G; t < nt; t += NW) {
-                uint4 u = buf[(t * 2 + 0) * 64 + lane];
-                uint4 v = buf[(t * 2 + 1) * 64 + lane];
-                uint32_t W[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
-                tr8(W, m4, m2, m1);
-                buf[(t * 2 + 0) * 64 + lane] = make_uint4(W[0], W[1], W[2], W[3]);
-                buf[(t * 2 + 1) * 64 + lane] = make_uint4(W[4], W[5], W[6], W[7]);
-            }
-            FP_MARK(2);
-            barrier_lds();
-            FP_MARK(3);
-            tc_chunk<NW>(lds0 + (uint32_t)((n & 1) * S * 2 * 64 * 16) + lane * 16,
-                         sp + (size_t)(n * S) * (NW * 8), nt);
-            FP_MARK(4);
-            barrier_lds();  // buffer n & 1 is refilled by part n + 2
-        }
-        FP_MARK(5);
-    } else {
-    auto first_src = [&](int n) { return (NCH - 1 - n / NP) * C + (n % NP) * S; };
-    auto part_len = [&](int n) { return min(S, C - (n % NP) * S); };
-    // The live sources of step n are dealt round-robin over the waves by
-    // rank (starting at wave n % NW), so every wave moves and transposes
-    // the same number of rows, +-1, whatever the erasure pattern.
-    auto live_bits = [&](int n) -> uint32_t {  // bit t: slot t of step n is a live source
-        const int j0 = first_src(n);
-        const int nt = min(part_len(n), K - j0);  // slots past K hold nothing
-        const uint64_t er = j0 == 0 ? em0 : j0 < 64 ? (em0 >> j0) | (em1 << (64 - j0)) : em1 >> (j0 - 64);
-        return ~(uint32_t)er & ((1u << nt) - 1);  // nt <= S = 8
+        const uint64_t lv0 = ~em0 & range(0, K), lv1 = ~em1 & range(0, K - 64);
+        for (int j = lane; j < K; j += 64)
+            if (live(j))
+                items[__popcll(lv0 & range(0, j)) + __popcll(lv1 & range(-64, j - 64))] = (uint8_t)j;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // own lanes' writes, in order
+        vi0 = lane < NL ? items[lane] : 0;
+        vi1 = 64 + lane < NL ? items[64 + lane] : 0;
+    }
+    auto survivor = [&](int q) -> int {
+        return __builtin_amdgcn_readlane((int)(q < 64 ? vi0 : vi1), q & 63);
     };
-    auto dealt = [&](int n, uint32_t m) -> uint32_t {  // this wave's slots of step n
-        uint32_t mine = 0;
-        for (int rk = n % NW; m; m &= m - 1, rk = rk + 1 == NW ? 0 : rk + 1)
-            mine |= rk == G ? m & (0u - m) : 0u;
-        return mine;
-    };
-    auto issue1 = [&](int n, uint32_t mine) {
-        const int j0 = first_src(n);
+    auto part_n = [&](int n) { return min(S, NL - n * S); };
+    auto issue1 = [&](int n) {
         const uint32_t base = lds0 + (uint32_t)((n & 1) * S * 2 * 64 * 16);
-        for (; mine; mine &= mine - 1) {
-            const int t = __builtin_ctz(mine);
-            glds32(sb + (size_t)(j0 + t) * a.pitch, (uint32_t)loff, base + (uint32_t)(t * 2 * 64 * 16));
-        }
+        for (int t = G; t < part_n(n); t += NW)
+            glds32(sb + (size_t)survivor(n * S + t) * a.pitch, (uint32_t)loff,
+                   base + (uint32_t)(t * 2 * 64 * 16));
     };
-    auto issued1 = [&](uint32_t mine) { return 2 * __builtin_popcount(mine); };
-
-    // Parity rows straight into this wave's accumulators; their latency
-    // overlaps the first two LDS-DMA parts.  (Streaming one parity row per
-    // step instead, scaled for the twiddles still to come, removed this
-    // prologue but measured 1-2 % slower overall.)
+    auto own1 = [&](int n) {
+        const int nt = part_n(n);
+        return nt > G ? 2 * ((nt - G + NW - 1) / NW) : 0;
+    };
     asm volatile(RSGPU_TC_ZERO ::: RSGPU_TC_ACC_CLOBBERS);
+    // parity rows straight into this wave's accumulators (unscaled)
     [&]<int... Ss>(std::integer_sequence<int, Ss...>) {
         ((G * 8 + Ss < E ? load_slot<Ss>(a.par + ((size_t)b * E + G * 8 + Ss) * a.pitch + loff)
                          : void()),
          ...);
     }(std::make_integer_sequence<int, 8>{});
-    uint32_t mine_next = dealt(0, live_bits(0));
-    issue1(0, mine_next);
-    // buffer 1 is free from the start: part 1 flies during the parity work
-    const uint32_t mine1 = NSTEP > 1 ? dealt(1, live_bits(1)) : 0u;
+    issue1(0);  // NL >= 1 (rs_decode_fused_available)
     if (NSTEP > 1)
-        issue1(1, mine1);
-    wait_vm(issued1(mine_next) + issued1(mine1));  // the (older) parity loads have landed
-    // bytes -> planes, scaled by 2^(-C r (NCH-1)): the NCH-1 Horner twiddles
-    // of the chunk loop bring them back to P_r
+        issue1(1);
+    wait_vm(own1(0) + (NSTEP > 1 ? own1(1) : 0));  // the (older) parity loads have landed
     [&]<int... Ss>(std::integer_sequence<int, Ss...>) {
         (
             [&] {
@@ -424,28 +257,24 @@ __device__ __forceinline__ void run_group(const Args& a, uint4 (*lds)[S * 2 * 64
             }(),
             ...);
     }(std::make_integer_sequence<int, 8>{});
-    syn_prescale<K, E, C, NW>(G);
     FP_MARK(12);
+    const unsigned long long* sp = a.syn_addr + (size_t)b * NL * (NW * 8) + G * 8;
     for (int n = 0; n < NSTEP; ++n) {
-        uint4* buf = lds[n & 1];
-        const int j0 = first_src(n);
-        const uint32_t mine = mine_next;
+        const int nt = part_n(n);
         FP_MARK(5);
-        if (n == 0 && NSTEP > 1) {  // part 1 already issued in the prologue
-            mine_next = mine1;
+        if (n == 0) {
             FP_MARK(0);
-            wait_vm(issued1(mine_next));
+            wait_vm(NSTEP > 1 ? own1(1) : 0);
         } else if (n + 1 < NSTEP) {
-            mine_next = dealt(n + 1, live_bits(n + 1));
-            issue1(n + 1, mine_next);
+            issue1(n + 1);
             FP_MARK(0);
-            wait_vm(issued1(mine_next));
+            wait_vm(own1(n + 1));
         } else {
             wait_vm(0);
         }
         FP_MARK(1);
-        for (uint32_t mm = mine; mm; mm &= mm - 1) {
-            const int t = __builtin_ctz(mm);
+        uint4* buf = lds[n & 1];
+        for (int t = G; t < nt; t += NW) {
             uint4 u = buf[(t * 2 + 0) * 64 + lane];
             uint4 v = buf[(t * 2 + 1) * 64 + lane];
             uint32_t W[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
@@ -456,18 +285,12 @@ __device__ __forceinline__ void run_group(const Args& a, uint4 (*lds)[S * 2 * 64
         FP_MARK(2);
         barrier_lds();
         FP_MARK(3);
-        const int part = n % NP;
-        if (part == 0 && n != 0)
-            syn_twiddle<K, E, C, NW>(G);
-        [&]<int... Ps>(std::integer_sequence<int, Ps...>) {
-            ((part == Ps ? syn_part<K, C, E, NW, Ps>(G, buf, lane, j0, em0, em1) : void()), ...);
-        }(std::make_integer_sequence<int, NP>{});
+        tc_chunk<NW>(lds0 + (uint32_t)((n & 1) * S * 2 * 64 * 16) + lane * 16,
+                     sp + (size_t)(n * S) * (NW * 8), nt);
         FP_MARK(4);
-        barrier_lds();
+        barrier_lds();  // buffer n & 1 is refilled by part n + 2
     }
     FP_MARK(5);
-
-    }
 
     // The syndromes (parity included), in plane form, are phase 2's sources:
     // wave G's rows are its chunk G.  Waves 0 and 1 write theirs straight
@@ -497,7 +320,7 @@ __device__ __forceinline__ void run_group(const Args& a, uint4 (*lds)[S * 2 * 64
     FP_MARK(6);
 
     // ---------------- phase 2: x = V_E^-1 s (threaded code) ----------------
-    constexpr int NCH2 = (E + S - 1) / S;
+    const int NCH2 = (E + S - 1) / S;
     const unsigned long long* ap = a.addr + (size_t)b * E * (NW * 8) + G * 8;
     auto issue2 = [&](int ch) {
         const int c0 = ch * S, nt = min(S, E - c0);
@@ -529,7 +352,7 @@ __device__ __forceinline__ void run_group(const Args& a, uint4 (*lds)[S * 2 * 64
         FP_MARK(8);
         const uint32_t la = lds0 + (uint32_t)((ch & 1) * S * 2 * 64 * 16) + lane * 16;
         const unsigned long long* pa = ap + (size_t)(ch * S) * (NW * 8);
-tc_chunk<NW>(la, pa, nt);
+        tc_chunk<NW>(la, pa, nt);
         FP_MARK(9);
         if (ch == 0 && G >= NLDS)  // parked syndromes written before chunk NLDS is fetched
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -560,50 +383,25 @@ tc_chunk<NW>(la, pa, nt);
     FP_END;
 }
 
-template <int K, int E, int C, bool TC1>
-__global__ __launch_bounds__(64 * ((E + 7) / 8)) __attribute__((amdgpu_num_vgpr(64))) void
+template <int NW>
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_num_vgpr(64))) void
 k_rs_decode_fused(Args a)
 {
-    constexpr int NW = (E + 7) / 8;
     __shared__ uint4 lds[2][S * 2 * 64];
-    __shared__ uint8_t items[NW][128];  // per-wave survivor list (TC1)
+    __shared__ uint8_t items[NW][128];  // per-wave survivor list
     if (a.status[blockIdx.y] != 0)
         return;  // singular or malformed: the whole block is skipped
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    run_group<K, E, C, NW, TC1>(a, lds, items[wave], wave);
-}
-
-// Syndrome phase: threaded code (default) or the compile-time Horner blocks
-// (RSGPU_FUSED_SYN=horner, kept for comparison).
-bool fused_syn_tc()
-{
-    static const bool tc = [] {
-        const char* v = std::getenv("RSGPU_FUSED_SYN");
-        return !(v && std::strcmp(v, "horner") == 0);
-    }();
-    return tc;
-}
-
-template <int K, int E, int C>
-hipError_t launch(const Args& a, long long blocks, hipStream_t st)
-{
-    dim3 grid((unsigned)((a.len + 2047) / 2048), (unsigned)blocks);
-    if (fused_syn_tc() && a.syn_addr)
-        hipLaunchKernelGGL((k_rs_decode_fused<K, E, C, true>), grid, dim3(64 * ((E + 7) / 8)), 0,
-                           st, a);
-    else
-        hipLaunchKernelGGL((k_rs_decode_fused<K, E, C, false>), grid, dim3(64 * ((E + 7) / 8)), 0,
-                           st, a);
-    return hipGetLastError();
+    run_group<NW>(a, lds, items[wave], wave);
 }
 
 }  // namespace fused
 
+// any gf_gen_rs_matrix code with 1 <= e <= 32 parity rows, k <= 128 (the
+// survivor list is two lanes' words) and at least one surviving original
 bool rs_decode_fused_available(int k, int e)
 {
-    return (k == 16 && e == 4) || (k == 16 && e == 8) || (k == 64 && e == 32) ||
-           (k == 64 && e == 16) || (k == 100 && e == 20) || (k == 5 && e == 4) ||
-           (k == 20 && e == 7);
+    return e >= 1 && e <= 32 && k <= 128 && k > e;
 }
 
 hipError_t launch_rs_decode_fused(int k, int e, const uint8_t* src, const uint8_t* par,
@@ -612,15 +410,17 @@ hipError_t launch_rs_decode_fused(int k, int e, const uint8_t* src, const uint8_
                                   const unsigned long long* syn_addr, const int* status,
                                   hipStream_t st)
 {
-    fused::Args a{src, par, out, pitch, len, emask, addr, syn_addr, status};
-    if (k == 16 && e == 4) return fused::launch<16, 4, 8>(a, blocks, st);
-    if (k == 16 && e == 8) return fused::launch<16, 8, 8>(a, blocks, st);
-    if (k == 64 && e == 32) return fused::launch<64, 32, 8>(a, blocks, st);
-    if (k == 64 && e == 16) return fused::launch<64, 16, 8>(a, blocks, st);
-    if (k == 100 && e == 20) return fused::launch<100, 20, 8>(a, blocks, st);
-    if (k == 5 && e == 4) return fused::launch<5, 4, 5>(a, blocks, st);
-    if (k == 20 && e == 7) return fused::launch<20, 7, 8>(a, blocks, st);
-    return hipErrorInvalidValue;
+    if (!rs_decode_fused_available(k, e) || !syn_addr)
+        return hipErrorInvalidValue;
+    fused::Args a{src, par, out, k, e, pitch, len, emask, addr, syn_addr, status};
+    dim3 grid((unsigned)((len + 2047) / 2048), (unsigned)blocks);
+    switch ((e + 7) / 8) {
+    case 1: hipLaunchKernelGGL(fused::k_rs_decode_fused<1>, grid, dim3(64), 0, st, a); break;
+    case 2: hipLaunchKernelGGL(fused::k_rs_decode_fused<2>, grid, dim3(128), 0, st, a); break;
+    case 3: hipLaunchKernelGGL(fused::k_rs_decode_fused<3>, grid, dim3(192), 0, st, a); break;
+    default: hipLaunchKernelGGL(fused::k_rs_decode_fused<4>, grid, dim3(256), 0, st, a); break;
+    }
+    return hipGetLastError();
 }
 
 }  // namespace rsgpu

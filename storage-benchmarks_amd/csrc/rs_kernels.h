@@ -18,22 +18,31 @@ struct DotArgs {
     bool bytewise;                // pointers not 8-byte aligned: byte kernel
 };
 
+// General decode preparation (k_decode_prepare, one workgroup per block):
+// survivors = the first k rows of the m-row code not erased (ascending),
+// their k x k matrix inverted (Gauss-Jordan, isa/ec_base.c:99-152), with the
+// reference's retry when singular (erasure_code_base_test.c:163-184); decode
+// rows = inverse rows of erased data rows, encode row x inverse for erased
+// parity rows (:197-210).
 struct PrepArgs {
-    int k, e, rows_pad;
+    int k, m, nerrs, rows_pad;
     long long blocks;
-    const uint8_t* err;           // device [blocks][e]
-    const uint8_t* src; long long src_pitch;
-    const uint8_t* par; long long par_pitch;
-    uint8_t* out; long long out_pitch;
+    const uint8_t* err;           // device [blocks][nerrs], strictly ascending, < m
+    const uint8_t* enc;           // device m x k encode matrix, nullptr = gf_gen_rs_matrix(m, k)
+    int originals_only;           // isa_decoder form: every erased index must be < k
+    const uint8_t* src; long long src_pitch;   // [blocks][k] rows
+    const uint8_t* par; long long par_pitch;   // [blocks][m - k] rows
+    uint8_t* out; long long out_pitch;         // [blocks][nerrs] rows
     const uint8_t** surv_ptrs;    // device [blocks][k]
-    uint8_t** out_ptrs;           // device [blocks][e]
+    uint8_t** out_ptrs;           // device [blocks][nerrs]
     uint4* tabs4; uint32_t* ctab; long long tab_block_stride;  // v_perm tables, or nullptr
     int* status;                  // device [blocks]
     // k_rs_tc instead of k_dot_generic (when non-null): the context's
-    // 512-entry handler table and the [blocks][k][tc_rows] address output
+    // 2048-entry handler table and the address output, tc_block_stride
+    // elements per block in the pass layout of tc_table_elems()
     const unsigned long long* tc_table = nullptr;
     unsigned long long* tc_addr = nullptr;
-    int tc_rows = 0;
+    long long tc_block_stride = 0;
 };
 
 int generic_rows_per_pass(int rows);
@@ -49,52 +58,70 @@ hipError_t launch_fill_synth(uint8_t* dst, long long rows, long long len, long l
 hipError_t launch_compare_rows(const uint8_t* src, long long src_pitch, int k, const uint8_t* out,
                                long long out_pitch, int e, const uint8_t* err, long long len,
                                long long blocks, unsigned long long* mismatches, hipStream_t st);
-// Bit-sliced RS(k, e) with compile-time coefficients (rs_bitsliced.hip).
-// emask == nullptr: parity of the gf_gen_rs_matrix code into `out`.
-// emask != nullptr ([blocks][2] bitmask of erased originals): syndromes
-//   out[p] = par[p] ^ sum_{j not erased} 2^(p j) src[j].
-// Requires len % 32 == 0, 16-byte aligned rows.
+// Bit-sliced RS(k, e) parity of the gf_gen_rs_matrix code with compile-time
+// coefficients (rs_bitsliced.hip).  Requires len % 32 == 0, 16-byte aligned
+// rows.
 bool rs_bitsliced_available(int k, int e);
-hipError_t launch_rs_bitsliced(int k, int e, const uint8_t* src, const uint8_t* par, uint8_t* out,
-                               long long pitch, long long len, long long blocks,
-                               const uint64_t* emask, hipStream_t st);
+hipError_t launch_rs_bitsliced(int k, int e, const uint8_t* src, uint8_t* out, long long pitch,
+                               long long len, long long blocks, hipStream_t st);
 
-// Syndrome-decode prepare: per block, emask, V_E^-1 and its consumers' tables:
-// k_dot_generic tables (tabs4/ctab, when non-null) and/or k_rs_tc handler
-// addresses (tc_addr [B][e][tc_rows], when non-null; tc_table = the 256
-// handler addresses).  syn_addr (non-null with tc_table): [B][k-e][tc_rows]
-// handler addresses of the syndrome rows 2^(r j) per surviving original j
-// (ascending), for the fused decode's threaded-code syndrome phase.
-// dir_addr (non-null with tc_table): the one-matrix decode through k_rs_tc --
-// srcs [B][k] = surviving originals (ascending) then the e parity rows (from
-// src / par), dsts [B][e] = out rows, dir_addr [B][k][tc_rows] = handler
-// addresses of the e x k decode rows V_E^-1 [V_kept | I].
-hipError_t launch_decode_prepare_syn(int k, int e, int rows_pad, long long blocks,
-                                     const uint8_t* err, uint8_t* out, long long out_pitch,
-                                     const uint8_t** srcs, uint8_t** dsts, uint4* tabs4,
-                                     uint32_t* ctab, long long tab_block_stride,
-                                     const unsigned long long* tc_table,
-                                     unsigned long long* tc_addr, int tc_rows,
-                                     unsigned long long* emask, int* status,
-                                     unsigned long long* syn_addr, const uint8_t* src,
-                                     const uint8_t* par, unsigned long long* dir_addr,
-                                     hipStream_t st);
+// Syndrome-form decode prepare for the gf_gen_rs_matrix code with e erased
+// originals and all e parity rows surviving (e <= 32), per block: erasure
+// list validation (strictly ascending, < k; else status -2), emask [B][2],
+// and one of
+//   dir_addr != nullptr  the one-matrix decode through k_rs_tc: srcs [B][k]
+//                        = surviving originals (ascending) then the e parity
+//                        rows, dsts [B][e] = out rows, dir_addr [B][k][slots]
+//                        = handler addresses of the e x k decode rows
+//                        V_E^-1 [V_kept | I] (closed form, no elimination)
+//   otherwise            the fused decode's tables: tc_addr [B][e][slots]
+//                        handler addresses of V_E^-1 (e x e Gauss-Jordan) and
+//                        syn_addr [B][k-e][slots] of the syndrome rows
+//                        2^(r j) per surviving original j (ascending)
+// slots = tc_rows_per_pass(e); tc_table = the context's handler addresses.
+hipError_t launch_decode_prepare_syn(int k, int e, long long blocks, const uint8_t* err,
+                                     uint8_t* out, long long out_pitch, const uint8_t** srcs,
+                                     uint8_t** dsts, const unsigned long long* tc_table,
+                                     unsigned long long* tc_addr, unsigned long long* emask,
+                                     int* status, unsigned long long* syn_addr,
+                                     const uint8_t* src, const uint8_t* par,
+                                     unsigned long long* dir_addr, hipStream_t st);
 
 // Threaded-code bit-sliced dot product with runtime coefficients (rs_tc.hip):
-// dsts[b][i] = sum_p c_b[i][p] * srcs[b][p] for rows <= 32, where the
-// coefficients arrive as handler addresses addr[b][p][slot] (slot < tc_rows,
-// padding slots point at handler 0).  len % 32 == 0, 16-byte aligned rows;
-// blocks with status != 0 are skipped.
+// dsts[b][i] = sum_p c_b[i][p] * srcs[b][p] for rows <= 32 per launch, where
+// the coefficients arrive as handler addresses addr[b][p][slot] (slot <
+// tc_rows_per_pass(rows), padding slots point at handler 0).  len % 32 == 0,
+// 16-byte aligned rows; blocks with status != 0 are skipped.  More than 32
+// rows run as passes of 32 (the address tables in the pass layout below).
 struct TcArgs {
     const uint8_t* const* srcs;      // [B][k]
-    uint8_t* const* dsts;            // [B][rows]
+    uint8_t* const* dsts;            // [B][dst_stride], this launch's rows first
+    int dst_stride;                  // row pointers per block in dsts
     const unsigned long long* addr;  // [B][k][tc_rows_per_pass(rows)]
     long long addr_stride;           // elements between blocks' tables (0: shared)
     int k, rows;
     long long len;
     const int* status;               // [B] or nullptr
 };
-int tc_rows_per_pass(int rows);
+// slots of a pass of rows <= 32: rows rounded up to 8
+__host__ __device__ inline int tc_rows_per_pass(int rows) { return rows <= 0 ? 8 : (rows + 7) / 8 * 8; }
+// Pass layout of a handler-address table for `rows` output rows over k
+// sources: pass p (rows 32p .. 32p+31) at element offset tc_pass_offset,
+// [k][tc_rows_per_pass(pass rows)] each; tc_table_elems in total.
+__host__ __device__ inline int tc_passes(int rows) { return rows <= 0 ? 1 : (rows + 31) / 32; }
+__host__ __device__ inline int tc_pass_rows(int rows, int p) { return rows - 32 * p < 32 ? rows - 32 * p : 32; }
+__host__ __device__ inline long long tc_pass_offset(int k, int p) { return (long long)k * 32 * p; }
+__host__ __device__ inline long long tc_table_elems(int k, int rows)
+{
+    const int np = tc_passes(rows);
+    return tc_pass_offset(k, np - 1) + (long long)k * tc_rows_per_pass(tc_pass_rows(rows, np - 1));
+}
+// element of (output row r, source j) in a pass-layout table
+__host__ __device__ inline long long tc_elem(int k, int rows, int r, int j)
+{
+    const int p = r / 32;
+    return tc_pass_offset(k, p) + (long long)j * tc_rows_per_pass(tc_pass_rows(rows, p)) + (r & 31);
+}
 
 // One-pass syndrome decode (rs_decode_fused.hip) for the instantiated
 // gf_gen_rs_matrix codes: out[b] = data rows listed by the prepare kernel's

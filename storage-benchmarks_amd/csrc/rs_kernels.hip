@@ -21,7 +21,11 @@
 //                     coefficient costs one v_bitop3 (acc ^= L[c&15] ^ H[c>>4]).
 //   k_decode_prepare  one workgroup per block: survivor rows -> k x k matrix
 //                     -> GF Gauss-Jordan inversion in LDS (isa/ec_base.c:99-152
-//                     semantics) -> decode rows -> v_perm tables + row pointers.
+//                     semantics, with gf_gen_decode_matrix's retry) -> decode
+//                     rows (data and parity erasures) -> k_rs_tc handler
+//                     addresses or v_perm tables + row pointers.
+//   k_decode_prepare_syn  the closed-form decode rows of the isa_throughput
+//                     case (erased originals, all parity rows surviving).
 //   k_fill_synth      seeded synthetic symbols (counter-based, see rs_synth.h).
 //   k_compare_rows    verify_data (isa.cpp:215-229) on the device.
 #include <hip/hip_runtime.h>
@@ -331,41 +335,32 @@ __global__ __launch_bounds__(256) void k_rs_encode_lh(const uint8_t* __restrict_
 }
 
 // ---------------------------------------------------------------------------
-// Decode preparation: one workgroup per block
+// Decode preparation: one workgroup per block (PrepArgs, rs_kernels.h)
 // ---------------------------------------------------------------------------
-// err:    [B][e] erased ORIGINAL indices, ascending (isa.cpp:150-153)
-// Produces per block: status (0 / -1 singular), survivor row pointers [k],
-// output row pointers [e], v_perm tables [k][rows_pad][5] of the decode rows
-// c[i][j] = inv(b)[err[i]][j] (isa.cpp:177-204).
-// LDS: two k x k byte matrices + log/antilog tables.
+// Per block: status (0; -1 singular, "BAD MATRIX"; -2 malformed erasure
+// list), survivor row pointers [k], output row pointers [nerrs], and the
+// decode rows as k_rs_tc handler addresses (pass layout) or v_perm tables
+// [k][rows_pad][5].  LDS: log / antilog, the erasure flags, the survivor
+// list and two k x k byte matrices.
 
 // log / antilog tables of GF(2^8), a compile-time constant (gf256.h)
 __device__ const GfTables kGfTables = make_gf_tables();
 
-__global__ __launch_bounds__(256) void k_decode_prepare(int k, int e, int rows_pad,
-                                                        const uint8_t* __restrict__ err,
-                                                        const uint8_t* src, long long src_pitch,
-                                                        const uint8_t* par, long long par_pitch,
-                                                        uint8_t* out, long long out_pitch,
-                                                        const uint8_t** surv_ptrs,
-                                                        uint8_t** out_ptrs, uint4* tabs4,
-                                                        uint32_t* ctab, long long tab_block_stride,
-                                                        int* status,
-                                                        const unsigned long long* tc_table,
-                                                        unsigned long long* tc_addr, int tc_rows)
+__global__ __launch_bounds__(256) void k_decode_prepare(PrepArgs a)
 {
     extern __shared__ __align__(16) uint8_t lds[];
     uint8_t* gexp = lds;             // 512
     uint8_t* glog = lds + 512;       // 256
     uint8_t* in_err = lds + 768;     // 256
-    uint8_t* surv = lds + 1024;      // 256
+    uint8_t* surv = lds + 1024;      // 256: decode_index (erasure_code_base_test.c:156-162)
     int* sh = reinterpret_cast<int*>(lds + 1280);  // 16 ints
+    const int k = a.k, m = a.m, ne = a.nerrs;
     uint8_t* A = lds + 1344;         // k*k
     uint8_t* Dm = A + k * k;         // k*k
 
     const int b = blockIdx.x;
     const int tid = threadIdx.x, nt = blockDim.x;
-    const int m = k + e;
+    const uint8_t* eb = a.err + (size_t)b * ne;
 
     for (int i = tid; i < 512; i += nt) {
         gexp[i] = kGfTables.exp[i];
@@ -375,145 +370,197 @@ __global__ __launch_bounds__(256) void k_decode_prepare(int k, int e, int rows_p
     for (int i = tid; i < 256; i += nt)
         in_err[i] = 0;
     __syncthreads();
-    const uint8_t* eb = err + (size_t)b * e;
-    for (int i = tid; i < e; i += nt)
-        in_err[eb[i]] = 1;
-    __syncthreads();
     if (tid == 0) {
-        // survivors: ascending encode-row index skipping erased (isa.cpp:177-182)
-        int r = 0, bad = 0;
-        for (int i = 0; i < k; ++i, ++r) {
-            while (r < m && in_err[r])
-                ++r;
-            if (r >= m) {  // malformed erasure list (duplicates / out of range)
-                bad = 1;
-                r = 0;
-            }
-            surv[i] = (uint8_t)r;
+        // validate: strictly ascending, < m (< k for the isa_decoder form),
+        // at most m - k erasures (k survivors must exist)
+        int bad = ne > m - k;
+        int nsrc = 0;
+        for (int i = 0; i < ne; ++i) {
+            const int j = eb[i];
+            bad |= j >= m || (a.originals_only && j >= k) || (i > 0 && j <= eb[i - 1]);
+            nsrc += j < k;
         }
-        for (int i = 0; i < e; ++i)
-            bad |= (eb[i] >= k);
+        if (!bad) {
+            for (int i = 0; i < ne; ++i)
+                in_err[eb[i]] = 1;
+            // survivors: the first k rows not erased, ascending (isa.cpp:177-
+            // 182; erasure_code_base_test.c:156-162)
+            int r = 0;
+            for (int i = 0; i < k; ++i, ++r) {
+                while (in_err[r])
+                    ++r;
+                surv[i] = (uint8_t)r;
+            }
+        }
         sh[0] = bad ? -2 : 0;
+        sh[2] = nsrc;  // nsrcerrs: the data erasures come first (ascending)
+        sh[3] = 0;     // incr of the retry loop
     }
     __syncthreads();
     if (sh[0] != 0) {
         if (tid == 0)
-            status[b] = sh[0];
+            a.status[b] = sh[0];
         return;
     }
-    // b[i][j] = a[surv[i]][j], a = gf_gen_rs_matrix(m, k)
-    for (int idx = tid; idx < k * k; idx += nt) {
-        const int i = idx / k, j = idx - i * k;
-        const int r = surv[i];
-        uint8_t v;
-        if (r < k)
-            v = (r == j) ? 1 : 0;
-        else {
-            const int p = r - k;
-            v = gexp[(p * j) % 255];
-        }
-        A[idx] = v;
-        Dm[idx] = (i == j) ? 1 : 0;
-    }
-    __syncthreads();
     auto gmul = [&](uint8_t x, uint8_t y) -> uint8_t {
         return (x && y) ? gexp[glog[x] + glog[y]] : (uint8_t)0;
     };
-    // Gauss-Jordan (isa/ec_base.c:99-152): zero pivot -> swap with the first
-    // lower row holding a non-zero in that column; singular -> -1.
-    for (int i = 0; i < k; ++i) {
-        if (tid == 0) {
-            int piv = i;
-            if (A[i * k + i] == 0) {
-                piv = -1;
-                for (int j = i + 1; j < k; ++j)
-                    if (A[j * k + i]) {
-                        piv = j;
-                        break;
-                    }
-            }
-            sh[1] = piv;
+    // encode-matrix entry (row r, column j): the caller's matrix, or
+    // gf_gen_rs_matrix (isa/ec_base.c:62-79: identity, then 2^(p j))
+    auto enc = [&](int r, int j) -> uint8_t {
+        if (a.enc)
+            return a.enc[(size_t)r * k + j];
+        if (r < k)
+            return r == j ? 1 : 0;
+        return gexp[((r - k) * j) % 255];
+    };
+    for (;;) {
+        // b[i][j] = encode row surv[i]
+        for (int idx = tid; idx < k * k; idx += nt) {
+            const int i = idx / k, j = idx - i * k;
+            A[idx] = enc(surv[i], j);
+            Dm[idx] = (i == j) ? 1 : 0;
         }
         __syncthreads();
-        const int piv = sh[1];
-        if (piv < 0) {
-            if (tid == 0)
-                sh[0] = -1;
-            break;
-        }
-        if (piv != i) {
+        // Gauss-Jordan (isa/ec_base.c:99-152): zero pivot -> swap with the
+        // first lower row holding a non-zero in that column; singular -> -1
+        int singular = 0;
+        for (int i = 0; i < k; ++i) {
+            if (tid == 0) {
+                int piv = i;
+                if (A[i * k + i] == 0) {
+                    piv = -1;
+                    for (int j = i + 1; j < k; ++j)
+                        if (A[j * k + i]) {
+                            piv = j;
+                            break;
+                        }
+                }
+                sh[1] = piv;
+            }
+            __syncthreads();
+            const int piv = sh[1];
+            if (piv < 0) {
+                singular = 1;
+                break;
+            }
+            if (piv != i) {
+                for (int c = tid; c < k; c += nt) {
+                    uint8_t t = A[i * k + c];
+                    A[i * k + c] = A[piv * k + c];
+                    A[piv * k + c] = t;
+                    t = Dm[i * k + c];
+                    Dm[i * k + c] = Dm[piv * k + c];
+                    Dm[piv * k + c] = t;
+                }
+                __syncthreads();
+            }
+            const uint8_t pinv = gexp[255 - glog[A[i * k + i]]];
+            __syncthreads();
             for (int c = tid; c < k; c += nt) {
-                uint8_t t = A[i * k + c];
-                A[i * k + c] = A[piv * k + c];
-                A[piv * k + c] = t;
-                t = Dm[i * k + c];
-                Dm[i * k + c] = Dm[piv * k + c];
-                Dm[piv * k + c] = t;
+                A[i * k + c] = gmul(A[i * k + c], pinv);
+                Dm[i * k + c] = gmul(Dm[i * k + c], pinv);
+            }
+            __syncthreads();
+            // eliminate column i from every other row; factor read before update
+            for (int idx = tid; idx < k * k; idx += nt) {
+                const int r = idx / k, c = idx - r * k;
+                if (r == i || c == i)
+                    continue;  // column i updated after the sweep
+                const uint8_t f = A[r * k + i];
+                A[idx] ^= gmul(f, A[i * k + c]);
+                Dm[idx] ^= gmul(f, Dm[i * k + c]);
+            }
+            __syncthreads();
+            for (int r = tid; r < k; r += nt) {
+                if (r == i)
+                    continue;
+                const uint8_t f = A[r * k + i];
+                // column i of Dm was handled in the sweep only for c != i
+                Dm[r * k + i] ^= gmul(f, Dm[i * k + i]);
+                A[r * k + i] = 0;
             }
             __syncthreads();
         }
-        const uint8_t pinv = gexp[255 - glog[A[i * k + i]]];
-        __syncthreads();
-        for (int c = tid; c < k; c += nt) {
-            A[i * k + c] = gmul(A[i * k + c], pinv);
-            Dm[i * k + c] = gmul(Dm[i * k + c], pinv);
+        if (!singular)
+            break;
+        // the reference's retry (erasure_code_base_test.c:163-184): with all
+        // m - k rows erased there is nothing to swap in ("BAD MATRIX");
+        // otherwise the last survivor moves `incr` rows further, stepping
+        // over erased parity rows listed in src_err_list[nsrcerrs ..
+        // nerrs - nsrcerrs) (the loop bound as written there)
+        if (tid == 0) {
+            int st = 0;
+            if (ne == m - k) {
+                st = -1;
+            } else {
+                int incr = sh[3] + 1;
+                const int nsrc = sh[2];
+                for (int i = nsrc; i < ne - nsrc; ++i)
+                    if (eb[i] == surv[k - 1] + incr)
+                        ++incr;
+                if (surv[k - 1] + incr >= m)
+                    st = -1;
+                else
+                    surv[k - 1] = (uint8_t)(surv[k - 1] + incr);
+                sh[3] = incr;
+            }
+            sh[0] = st;
         }
         __syncthreads();
-        // eliminate column i from every other row; factor read before update
-        for (int idx = tid; idx < k * k; idx += nt) {
-            const int r = idx / k, c = idx - r * k;
-            if (r == i)
-                continue;
-            const uint8_t f = A[r * k + i];
-            if (c == i)
-                continue;  // column i updated after the sweep
-            A[idx] ^= gmul(f, A[i * k + c]);
-            Dm[idx] ^= gmul(f, Dm[i * k + c]);
-        }
-        __syncthreads();
-        for (int r = tid; r < k; r += nt) {
-            if (r == i)
-                continue;
-            const uint8_t f = A[r * k + i];
-            // column i of Dm was handled in the sweep only for c != i
-            Dm[r * k + i] ^= gmul(f, Dm[i * k + i]);
-            A[r * k + i] = 0;
-        }
-        __syncthreads();
+        if (sh[0] != 0)
+            break;
     }
     __syncthreads();
     const int st = sh[0];
     if (tid == 0)
-        status[b] = st;
-    // pointers: survivors from the encoder's data / parity rows, outputs
-    for (int i = tid; i < k; i += nt) {
-        const int r = surv[i];
-        surv_ptrs[(size_t)b * k + i] = (r < k) ? src + ((size_t)b * k + r) * src_pitch
-                                               : par + ((size_t)b * e + (r - k)) * par_pitch;
-    }
-    for (int i = tid; i < e; i += nt)
-        out_ptrs[(size_t)b * e + i] = out + ((size_t)b * e + i) * out_pitch;
+        a.status[b] = st;
     if (st != 0)
         return;
-    if (tc_addr && tc_table) {
-        // k_rs_tc handler addresses [j][slot]: coefficient inv(b)[err[slot]][j]
-        // of survivor j (the isa.cpp:184-204 decode rows), padding slots ->
-        // handler 0; the table is [slot][coefficient]
-        unsigned long long* ta = tc_addr + (size_t)b * k * tc_rows;
-        for (int idx = tid; idx < k * tc_rows; idx += nt) {
-            const int j = idx / tc_rows, r = idx - j * tc_rows;
-            ta[idx] = tc_table[(r & 7) * 256 + (r < e ? Dm[eb[r] * k + j] : 0)];
+    // pointers: survivors from the data / parity rows, outputs
+    for (int i = tid; i < k; i += nt) {
+        const int r = surv[i];
+        a.surv_ptrs[(size_t)b * k + i] = (r < k) ? a.src + ((size_t)b * k + r) * a.src_pitch
+                                                 : a.par + ((size_t)b * (m - k) + (r - k)) * a.par_pitch;
+    }
+    for (int i = tid; i < ne; i += nt)
+        a.out_ptrs[(size_t)b * ne + i] = a.out + ((size_t)b * ne + i) * a.out_pitch;
+    // decode row i, survivor column j (erasure_code_base_test.c:197-210;
+    // isa.cpp:200-204): data erasures take row err[i] of inv(b); parity
+    // erasures the encode row times inv(b)
+    const int nsrc = sh[2];
+    auto coef = [&](int i, int j) -> uint8_t {
+        if (i < nsrc)
+            return Dm[eb[i] * k + j];
+        const int r = eb[i];
+        uint8_t s = 0;
+        for (int q = 0; q < k; ++q)
+            s ^= gmul(Dm[q * k + j], enc(r, q));
+        return s;
+    };
+    if (a.tc_addr && a.tc_table) {
+        // k_rs_tc handler addresses (pass layout), padding slots -> handler 0
+        unsigned long long* ta = a.tc_addr + (size_t)b * a.tc_block_stride;
+        const int np = tc_passes(ne);
+        for (int p = 0; p < np; ++p) {
+            const int pr = tc_pass_rows(ne, p), slots = tc_rows_per_pass(pr);
+            unsigned long long* tp = ta + tc_pass_offset(k, p);
+            for (int idx = tid; idx < k * slots; idx += nt) {
+                const int j = idx / slots, s = idx - j * slots;
+                tp[idx] = a.tc_table[(s & 7) * 256 + (s < pr ? coef(32 * p + s, j) : 0)];
+            }
         }
         return;
     }
-    // tables: [j][rows_pad], rows beyond e zero
-    uint4* t4 = tabs4 + (size_t)b * tab_block_stride;
-    uint32_t* tc = ctab + (size_t)b * tab_block_stride;
+    // v_perm tables: [j][rows_pad], rows beyond nerrs zero
+    uint4* t4 = a.tabs4 + (size_t)b * a.tab_block_stride;
+    uint32_t* tc = a.ctab + (size_t)b * a.tab_block_stride;
+    const int rows_pad = a.rows_pad;
     for (int idx = tid; idx < k * rows_pad; idx += nt) {
         const int j = idx / rows_pad, r = idx - j * rows_pad;
         uint32_t t[5] = {0, 0, 0, 0, 0};
-        if (r < e) {
-            const uint8_t c = Dm[eb[r] * k + j];
+        if (r < ne) {
+            const uint8_t c = coef(r, j);
             uint8_t v[20];
 #pragma unroll
             for (int n = 0; n < 8; ++n) {
@@ -531,7 +578,6 @@ __global__ __launch_bounds__(256) void k_decode_prepare(int k, int e, int rows_p
         t4[idx] = make_uint4(t[0], t[1], t[2], t[3]);
         tc[idx] = t[4];
     }
-    (void)m;
 }
 
 // ---------------------------------------------------------------------------
@@ -692,17 +738,16 @@ size_t decode_prepare_lds_bytes(int k) { return 1344 + 2 * (size_t)k * k; }
 
 hipError_t launch_decode_prepare(const PrepArgs& a, hipStream_t st)
 {
+    if (a.k <= 0 || a.k > 250 || a.m < a.k || a.m > 256 || a.nerrs <= 0)
+        return hipErrorInvalidValue;
     const size_t lds = decode_prepare_lds_bytes(a.k);
     static bool attr_set = false;
     if (!attr_set) {
         (void)hipFuncSetAttribute((const void*)k_decode_prepare,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attr_set = true;
     }
-    hipLaunchKernelGGL(k_decode_prepare, dim3((unsigned)a.blocks), dim3(256), lds, st, a.k, a.e,
-                       a.rows_pad, a.err, a.src, a.src_pitch, a.par, a.par_pitch, a.out,
-                       a.out_pitch, a.surv_ptrs, a.out_ptrs, a.tabs4, a.ctab,
-                       a.tab_block_stride, a.status, a.tc_table, a.tc_addr, a.tc_rows);
+    hipLaunchKernelGGL(k_decode_prepare, dim3((unsigned)a.blocks), dim3(256), lds, st, a);
     return hipGetLastError();
 }
 
@@ -819,14 +864,12 @@ hipError_t launch_update(const uint8_t* data, uint8_t* const* coding, const uint
 // Outputs: emask[b][2], srcs[b][e] = dsts[b][e] = out rows (the syndrome
 // kernel writes s into out; the dot product then runs in place), tables of
 // V_E^-1 as [p][rows_pad], status.
-__global__ __launch_bounds__(256) void k_decode_prepare_syn(int k, int e, int rows_pad,
+__global__ __launch_bounds__(256) void k_decode_prepare_syn(int k, int e,
                                                             const uint8_t* __restrict__ err,
                                                             uint8_t* out, long long out_pitch,
                                                             const uint8_t** srcs, uint8_t** dsts,
-                                                            uint4* tabs4, uint32_t* ctab,
-                                                            long long tab_block_stride,
                                                             const unsigned long long* tc_table,
-                                                            unsigned long long* tc_addr, int tc_rows,
+                                                            unsigned long long* tc_addr,
                                                             unsigned long long* emask, int* status,
                                                             unsigned long long* syn_addr,
                                                             const uint8_t* src, const uint8_t* par,
@@ -872,7 +915,8 @@ __global__ __launch_bounds__(256) void k_decode_prepare_syn(int k, int e, int ro
     auto gmul = [&](uint8_t x, uint8_t y) -> uint8_t {
         return (x && y) ? gexp[glog[x] + glog[y]] : (uint8_t)0;
     };
-    if (dir_addr && tc_table) {
+    const int tc_rows = tc_rows_per_pass(e);
+    if (dir_addr) {
         // One-matrix decode through k_rs_tc: sources = the k - e surviving
         // originals (ascending) then the e parity rows, outputs = the erased
         // originals.  d_E = V_E^-1 (P ^ V_kept d_kept), V_E[p][i] = a_i^p with
@@ -1032,16 +1076,9 @@ __global__ __launch_bounds__(256) void k_decode_prepare_syn(int k, int e, int ro
     const int st = sh[0];
     if (tid == 0)
         status[b] = st;
-    if (!dir_addr) {
-        for (int i = tid; i < e; i += nt) {
-            uint8_t* row = out + ((size_t)b * e + i) * out_pitch;
-            srcs[(size_t)b * e + i] = row;
-            dsts[(size_t)b * e + i] = row;
-        }
-    }
     if (st != 0)
         return;
-    if (syn_addr && tc_table) {
+    {
         // syndrome phase of the fused decode (threaded code): the q-th
         // surviving original j_q (ascending) carries coefficient 2^(r j_q)
         // for syndrome row r = slot (gf_gen_rs_matrix row k + r,
@@ -1064,7 +1101,7 @@ __global__ __launch_bounds__(256) void k_decode_prepare_syn(int k, int e, int ro
             sa[idx] = tc_table[(r & 7) * 256 + (r < e ? gexp[(r * (int)lv[q]) % 255] : 0)];
         }
     }
-    if (tc_addr) {
+    {
         // handler addresses [p][slot]: coefficient (V_E^-1)[slot][p], padding
         // slots -> handler 0 (no-op)
         unsigned long long* ta = tc_addr + (size_t)b * e * tc_rows;
@@ -1073,48 +1110,20 @@ __global__ __launch_bounds__(256) void k_decode_prepare_syn(int k, int e, int ro
             ta[idx] = tc_table[(i & 7) * 256 + (i < e ? Dm[i * n + p] : 0)];
         }
     }
-    if (!tabs4)
-        return;
-    // tables: source p (syndrome row), output i: coefficient (V_E^-1)[i][p]
-    uint4* t4 = tabs4 + (size_t)b * tab_block_stride;
-    uint32_t* tc = ctab + (size_t)b * tab_block_stride;
-    for (int idx = tid; idx < e * rows_pad; idx += nt) {
-        const int p = idx / rows_pad, i = idx - p * rows_pad;
-        uint32_t t[5] = {0, 0, 0, 0, 0};
-        if (i < e) {
-            const uint8_t c = Dm[i * n + p];
-            uint8_t v[20];
-#pragma unroll
-            for (int q = 0; q < 8; ++q) {
-                v[q] = gmul(c, (uint8_t)q);
-                v[8 + q] = gmul(c, (uint8_t)(q << 3));
-            }
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-                v[16 + q] = gmul(c, (uint8_t)(q << 6));
-#pragma unroll
-            for (int q = 0; q < 5; ++q)
-                t[q] = (uint32_t)v[4 * q] | ((uint32_t)v[4 * q + 1] << 8) |
-                       ((uint32_t)v[4 * q + 2] << 16) | ((uint32_t)v[4 * q + 3] << 24);
-        }
-        t4[idx] = make_uint4(t[0], t[1], t[2], t[3]);
-        tc[idx] = t[4];
-    }
 }
 
 size_t decode_prepare_syn_lds_bytes(int e) { return 832 + 2 * (size_t)e * e + 256 + 512; }
 
-hipError_t launch_decode_prepare_syn(int k, int e, int rows_pad, long long blocks,
-                                     const uint8_t* err, uint8_t* out, long long out_pitch,
-                                     const uint8_t** srcs, uint8_t** dsts, uint4* tabs4,
-                                     uint32_t* ctab, long long tab_block_stride,
-                                     const unsigned long long* tc_table,
-                                     unsigned long long* tc_addr, int tc_rows,
-                                     unsigned long long* emask, int* status,
-                                     unsigned long long* syn_addr, const uint8_t* src,
-                                     const uint8_t* par, unsigned long long* dir_addr,
-                                     hipStream_t st)
+hipError_t launch_decode_prepare_syn(int k, int e, long long blocks, const uint8_t* err,
+                                     uint8_t* out, long long out_pitch, const uint8_t** srcs,
+                                     uint8_t** dsts, const unsigned long long* tc_table,
+                                     unsigned long long* tc_addr, unsigned long long* emask,
+                                     int* status, unsigned long long* syn_addr,
+                                     const uint8_t* src, const uint8_t* par,
+                                     unsigned long long* dir_addr, hipStream_t st)
 {
+    if (k <= 0 || k > 250 || e <= 0 || e > 32 || !tc_table || (!dir_addr && (!tc_addr || !syn_addr)))
+        return hipErrorInvalidValue;
     static bool attr_set = false;
     if (!attr_set) {
         (void)hipFuncSetAttribute((const void*)k_decode_prepare_syn,
@@ -1122,9 +1131,8 @@ hipError_t launch_decode_prepare_syn(int k, int e, int rows_pad, long long block
         attr_set = true;
     }
     hipLaunchKernelGGL(k_decode_prepare_syn, dim3((unsigned)blocks), dim3(256),
-                       decode_prepare_syn_lds_bytes(e), st, k, e, rows_pad, err, out, out_pitch,
-                       srcs, dsts, tabs4, ctab, tab_block_stride, tc_table, tc_addr, tc_rows,
-                       emask, status, syn_addr, src, par, dir_addr);
+                       decode_prepare_syn_lds_bytes(e), st, k, e, err, out, out_pitch, srcs, dsts,
+                       tc_table, tc_addr, emask, status, syn_addr, src, par, dir_addr);
     return hipGetLastError();
 }
 

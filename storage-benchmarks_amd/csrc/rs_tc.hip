@@ -38,8 +38,6 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include <algorithm>
-#include <cstdlib>
 #include <utility>
 
 #include "bitslice.h"
@@ -146,11 +144,6 @@ __device__ __forceinline__ void read_slot(uint32_t (&W)[8])
 // amdgpu_num_vgpr(64): the compiler allocates v0..v63 only; the accumulators
 // v64..v127 are touched by asm alone, so they stay put across the loops (the
 // kernel descriptor still reserves 128 VGPRs because the asm names v127).
-// RSGPU_TC_ONEBAR: one barrier per step (the next step's LDS-DMA issued right
-// after this step's post-transpose barrier) instead of two.
-#ifndef RSGPU_TC_ONEBAR
-#define RSGPU_TC_ONEBAR 1
-#endif
 template <int NW>
 __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_num_vgpr(64))) void k_rs_tc(TcArgs a, int tiles_per_wg)
 {
@@ -169,17 +162,12 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_num_vgpr(64))) void 
     const int nch = (k + C - 1) / C;
     const int total = my_tiles * nch;  // (tile, chunk) steps, pipelined across tiles
     const uint8_t* const* srcs = a.srcs + (size_t)b * k;
-    uint8_t* const* dsts = a.dsts + (size_t)b * a.rows;
+    uint8_t* const* dsts = a.dsts + (size_t)b * a.dst_stride;
     // addresses [B][k][NW*8]: this wave's 8 slots of source j at ap + j*NW*8
     const unsigned long long* ap = a.addr + (size_t)b * a.addr_stride + wave * 8;
     const uint32_t m4 = vconst(0x0F0F0F0Fu), m2 = vconst(0x33333333u), m1 = vconst(0x55555555u);
     const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint4*)&lds[0][0];
 
-    // sources of chunk ch this wave moves: t = wave, wave + NW, ... < nt
-    auto own = [&](int ch) {
-        const int nt = min(C, k - ch * C);
-        return nt > wave ? (nt - wave + NW - 1) / NW : 0;
-    };
     auto issue = [&](int n) {
         const int ch = n % nch;
         const long long off = (tile0 + n / nch) * 2048 + lane * 32;
@@ -210,18 +198,8 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_num_vgpr(64))) void 
         const int nt = min(C, k - ch * C);
         uint4* buf = lds[n & 1];
         TC_PROF_MARK(6);
-#if RSGPU_TC_ONEBAR
         wait_vm(0);  // this step's own sources, issued behind the previous step's barrier
         TC_PROF_MARK(0);
-#else
-        if (n + 1 < total) {
-            issue(n + 1);  // lands while this chunk is transposed and consumed
-            TC_PROF_MARK(0);
-            wait_vm(2 * own((n + 1) % nch));
-        } else {
-            wait_vm(0);
-        }
-#endif
         TC_PROF_MARK(1);
         // own share of this chunk: bytes -> bit-planes, in place
         for (int t = wave; t < nt; t += NW) {
@@ -234,13 +212,11 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_num_vgpr(64))) void 
         }
         TC_PROF_MARK(2);
         barrier_lds();
-#if RSGPU_TC_ONEBAR
-        // every wave is past its dispatch of step n - 1, which read buffer
-        // (n + 1) & 1: the next step's sources may land there now and
-        // arrive during this step's dispatch
+        // one barrier per step: every wave is past its dispatch of step
+        // n - 1, which read buffer (n + 1) & 1, so the next step's sources
+        // may land there now and arrive during this step's dispatch
         if (n + 1 < total)
             issue(n + 1);
-#endif
         TC_PROF_MARK(3);
         if (ch == 0)
             asm volatile(RSGPU_TC_ZERO ::: RSGPU_TC_ACC_CLOBBERS);
@@ -289,9 +265,6 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_num_vgpr(64))) void 
             }
         }
         TC_PROF_MARK(5);
-#if !RSGPU_TC_ONEBAR
-        barrier_lds();  // buffer n & 1 is refilled by step n + 2
-#endif
     }
     TC_PROF_MARK(6);
     TC_PROF_END;
@@ -315,25 +288,17 @@ int tc_slot_copy(int slot)
     return copy[slot & 7];
 }
 
-int tc_rows_per_pass(int rows) { return rows <= 0 ? 8 : (rows + 7) / 8 * 8; }
-
 hipError_t launch_rs_tc(const TcArgs& a, long long blocks, hipStream_t st)
 {
     const int nw = tc_rows_per_pass(a.rows) / 8;
+    if (a.rows <= 0 || a.rows > 32 || a.k <= 0)
+        return hipErrorInvalidValue;
     const long long ntile = (a.len + 2047) / 2048;
-    // consecutive tiles per workgroup: the LDS-DMA pipeline runs across tile
-    // boundaries, so only the first chunk of a workgroup waits on HBM cold
-    int tpw = 1;
-    if (const char* v = std::getenv("RSGPU_TC_TILES"))
-        tpw = std::max(1, std::atoi(v));
-    while (tpw > 1 && ntile * blocks / tpw < 2048)  // keep >= 2048 workgroups
-        tpw /= 2;
-    dim3 grid((unsigned)((ntile + tpw - 1) / tpw), (unsigned)blocks);
-    // RSGPU_TC_LDS_PAD=bytes: extra dynamic LDS per workgroup, an occupancy
-    // experiment (fewer workgroups per CU); 0 by default
-    unsigned pad = 0;
-    if (const char* v = std::getenv("RSGPU_TC_LDS_PAD"))
-        pad = (unsigned)std::max(0, std::atoi(v));
+    // one 2 KB column tile per workgroup (several consecutive tiles per
+    // workgroup, the LDS-DMA pipeline running across them, measured equal)
+    const int tpw = 1;
+    const unsigned pad = 0;
+    dim3 grid((unsigned)ntile, (unsigned)blocks);
     switch (nw) {
     case 1: hipLaunchKernelGGL(tc::k_rs_tc<1>, grid, dim3(64), pad, st, a, tpw); break;
     case 2: hipLaunchKernelGGL(tc::k_rs_tc<2>, grid, dim3(128), pad, st, a, tpw); break;

@@ -18,17 +18,16 @@
 struct rsgpu_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
-    // second stream for the pipelined decode (syndrome chunk i+1 overlaps the
-    // solve of chunk i); created on first use, joined back into `stream`
-    hipStream_t aux = nullptr;
-    int decode_chunks = 1;
+    // cross-stream ordering events (rsgpu_set_stream), recycled round-robin
     std::vector<hipEvent_t> sync_evs;
     size_t sync_next = 0;
-    // threaded-code solve (rs_tc.hip): device table of the 256 handler
-    // addresses; tc_state 0 = not probed, 1 = ready, -1 = unavailable
+    // threaded-code kernel (rs_tc.hip): device table of the handler
+    // addresses [slot][coefficient]; tc_state 0 = not probed, 1 = ready,
+    // -1 = unavailable (k_dot_generic serves instead)
     unsigned long long* d_tc_table = nullptr;
-    unsigned long long h_tc_table[2048] = {};  // [slot][coefficient]
+    unsigned long long h_tc_table[2048] = {};
     int tc_state = 0;
+    int decode_kernel = RSGPU_DECODE_AUTO;
     std::string err;
     // grow-only device scratch for pointer tables / coefficient tables
     void* d_scratch = nullptr;
@@ -48,8 +47,6 @@ struct rsgpu_ctx {
     std::vector<Rec> recs;
     std::vector<hipEvent_t> ev_pool;
 };
-
-static bool use_tc(rsgpu_ctx* ctx, int e);
 
 namespace {
 
@@ -86,6 +83,10 @@ int fail(rsgpu_ctx* ctx, int code, const std::string& msg)
                         std::string(#call) + ": " + hipGetErrorString(e_));                   \
     } while (0)
 
+// Grow the scratch buffer.  Every kernel that may still read the old buffer
+// was enqueued on the context stream, or on an earlier stream the current
+// one waits on (rsgpu_set_stream), so synchronising the current stream
+// retires them all before the free.
 int ensure_scratch(rsgpu_ctx* ctx, size_t bytes)
 {
     if (ctx->scratch_bytes >= bytes)
@@ -159,24 +160,12 @@ hipEvent_t sync_event(rsgpu_ctx* ctx)
     return e;
 }
 
-// Number of block chunks for the two-stream decode: 1 (no overlap) for small
-// batches; RSGPU_DECODE_CHUNKS overrides for experiments.
-size_t decode_chunk_count(rsgpu_ctx* ctx, size_t blocks)
-{
-    size_t want = (size_t)ctx->decode_chunks;
-    if (const char* v = std::getenv("RSGPU_DECODE_CHUNKS"))
-        want = (size_t)std::max(1, std::atoi(v));
-    const size_t by_size = blocks / 32;  // keep >= 32 blocks per chunk
-    return std::max<size_t>(1, std::min(want, by_size));
-}
-
 // Brackets one kernel launch with events when timing is enabled.
 struct KTimer {
     rsgpu_ctx* ctx;
     hipStream_t s;
     rsgpu_ctx::Rec rec{};
-    KTimer(rsgpu_ctx* c, const char* name, size_t blocks, hipStream_t st = nullptr)
-        : ctx(c), s(st ? st : c->stream)
+    KTimer(rsgpu_ctx* c, const char* name, size_t blocks) : ctx(c), s(c->stream)
     {
         if (!ctx->timing)
             return;
@@ -195,21 +184,91 @@ struct KTimer {
     }
 };
 
-size_t tc_table_bytes(int k, int rows);
-void tc_fill_addr(const rsgpu_ctx* ctx, const uint8_t* coef, int k, int rows, unsigned long long* h);
-int tc_launch_shared(rsgpu_ctx* ctx, const unsigned long long* d_addr, int k, int rows, long long len,
-                     long long blocks, const uint8_t* const* d_srcs, uint8_t* const* d_dsts,
-                     const char* timer_name);
+// Locate the handler table of k_rs_tc once per context: the query kernel
+// reports the table's first and end addresses; the layout must be exactly
+// tc_handler_count() handlers of tc_handler_stride() bytes, otherwise the
+// threaded-code path stays off (and k_dot_generic serves).  The address
+// table has 2048 entries: [slot][coefficient], each the handler copy that
+// serves the slot (tc_slot_copy).
+int tc_init(rsgpu_ctx* ctx)
+{
+    if (ctx->tc_state != 0)
+        return ctx->tc_state;
+    ctx->tc_state = -1;
+    unsigned long long* d = nullptr;
+    if (hipMalloc((void**)&d, 2050 * sizeof(unsigned long long)) != hipSuccess)
+        return -1;
+    unsigned long long se[2] = {0, 0};
+    if (tc_query_handlers(d + 2048, ctx->stream) != hipSuccess ||
+        hipMemcpyAsync(se, d + 2048, sizeof se, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
+        hipStreamSynchronize(ctx->stream) != hipSuccess) {
+        (void)hipFree(d);
+        return -1;
+    }
+    const unsigned long long stride = (unsigned long long)tc_handler_stride();
+    const unsigned long long count = (unsigned long long)tc_handler_count();
+    if (se[0] == 0 || se[1] - se[0] != count * stride || count % 256 != 0 || count > 2048) {
+        std::fprintf(stderr, "rsgpu: threaded-code handler table has an unexpected layout "
+                             "(%#llx..%#llx); using k_dot_generic\n", se[0], se[1]);
+        (void)hipFree(d);
+        return -1;
+    }
+    unsigned long long h[2048];
+    for (int s = 0; s < 8; ++s)
+        for (int c = 0; c < 256; ++c)
+            h[s * 256 + c] = se[0] + (unsigned long long)(tc_slot_copy(s) * 256 + c) * stride;
+    if (hipMemcpy(d, h, sizeof h, hipMemcpyHostToDevice) != hipSuccess) {
+        (void)hipFree(d);
+        return -1;
+    }
+    std::memcpy(ctx->h_tc_table, h, sizeof h);
+    ctx->d_tc_table = d;
+    ctx->tc_state = 1;
+    return 1;
+}
 
-// Runtime-coefficient dot product through the threaded-code kernel: host
-// coefficients coef[rows][k] become one handler-address table [k][slots]
-// shared by every block (uploaded to scratch at tab_off); rows <= 32, len %
-// 32 == 0, 16-byte aligned rows behind the device pointer tables.
-int tc_from_host_coef(rsgpu_ctx* ctx, const uint8_t* coef, int k, int rows, long long len,
-                      long long blocks, const uint8_t* const* d_srcs, uint8_t* const* d_dsts,
-                      size_t tab_off, const char* timer_name);
+bool tc_ready(rsgpu_ctx* ctx) { return tc_init(ctx) == 1; }
 
-// Fill host tables [k][rows_pad] for coefficient matrix coef[rows][k]
+// Host-side handler addresses of coefficient matrix coef[rows][k] in the
+// pass layout (rs_kernels.h tc_elem): pass p, source j, slot s -> row 32p + s.
+void tc_fill_addr(const rsgpu_ctx* ctx, const uint8_t* coef, int k, int rows, unsigned long long* h)
+{
+    for (int p = 0; p < tc_passes(rows); ++p) {
+        const int pr = tc_pass_rows(rows, p), slots = tc_rows_per_pass(pr);
+        unsigned long long* hp = h + tc_pass_offset(k, p);
+        for (int j = 0; j < k; ++j)
+            for (int s = 0; s < slots; ++s)
+                hp[(size_t)j * slots + s] =
+                    ctx->h_tc_table[(s & 7) * 256 + (s < pr ? coef[(size_t)(32 * p + s) * k + j] : 0)];
+    }
+}
+
+// k_rs_tc over `rows` output rows as passes of <= 32 rows: d_srcs [B][k],
+// d_dsts [B][rows] device row-pointer tables, d_addr the pass-layout
+// handler addresses, addr_stride elements between blocks' tables (0: one
+// table shared by every block).
+int tc_launch(rsgpu_ctx* ctx, const char* name, const uint8_t* const* d_srcs, uint8_t* const* d_dsts,
+              const unsigned long long* d_addr, long long addr_stride, int k, int rows, long long len,
+              long long blocks, const int* d_status)
+{
+    for (int p = 0; p < tc_passes(rows); ++p) {
+        TcArgs t{};
+        t.srcs = d_srcs;
+        t.dsts = d_dsts + 32 * p;
+        t.dst_stride = rows;
+        t.addr = d_addr + tc_pass_offset(k, p);
+        t.addr_stride = addr_stride;
+        t.k = k;
+        t.rows = tc_pass_rows(rows, p);
+        t.len = len;
+        t.status = d_status;
+        KTimer kt(ctx, name, (size_t)blocks);
+        RS_HIP(ctx, launch_rs_tc(t, blocks, ctx->stream));
+    }
+    return RSGPU_OK;
+}
+
+// Fill host v_perm tables [k][rows_pad] for coefficient matrix coef[rows][k]
 // (coef row r column j at coef[r*k + j]).
 void fill_tables(const uint8_t* coef, int k, int rows, int rows_pad, uint4* t4, uint32_t* tc)
 {
@@ -229,32 +288,51 @@ int rows_pad_for(int rows)
     return (rows + R - 1) / R * R;
 }
 
-// Generic dot product launch from HOST coefficients coef[rows][k] over
-// device pointer tables already in place (d_srcs [blocks][k], d_dsts
-// [blocks][rows]).  Uploads the tables into scratch at offset `tab_off`.
-int generic_from_host_coef(rsgpu_ctx* ctx, const uint8_t* coef, int k, int rows, long long len,
-                           long long blocks, const uint8_t* const* d_srcs, uint8_t* const* d_dsts,
-                           size_t tab_off, bool bytewise)
+// Runtime-coefficient dot product from HOST coefficients coef[rows][k] over
+// device pointer tables (d_srcs [blocks][k], d_dsts [blocks][rows]), one
+// coefficient table shared by every block, uploaded into scratch at
+// tab_off: k_rs_tc for aligned 32-byte-multiple rows, otherwise
+// k_dot_generic.  `pre` (pre_bytes <= tab_off, optional) goes to the start
+// of scratch in the same upload (the pointer tables of ec_encode_data).
+int dot_from_host_coef(rsgpu_ctx* ctx, const uint8_t* coef, int k, int rows, long long len,
+                       long long blocks, const uint8_t* const* d_srcs, uint8_t* const* d_dsts,
+                       size_t tab_off, bool aligned, const char* tc_name,
+                       const void* pre = nullptr, size_t pre_bytes = 0)
 {
+    const bool tcp = aligned && len % 32 == 0 && tc_ready(ctx);
     const int rows_pad = rows_pad_for(rows);
     const size_t n = (size_t)k * rows_pad;
-    const size_t bytes4 = n * sizeof(uint4), bytesc = n * sizeof(uint32_t);
+    const size_t bytes = tcp ? sizeof(unsigned long long) * (size_t)tc_table_elems(k, rows)
+                             : n * (sizeof(uint4) + sizeof(uint32_t));
+    const size_t skip = pre ? tab_off : 0;  // staging offset of the table
     void* stage;
-    int rc = get_stage(ctx, bytes4 + bytesc, &stage);
+    int rc = get_stage(ctx, skip + bytes, &stage);
     if (rc)
         return rc;
-    uint4* t4 = (uint4*)stage;
-    uint32_t* tc = (uint32_t*)((char*)stage + bytes4);
-    fill_tables(coef, k, rows, rows_pad, t4, tc);
+    if (pre)
+        std::memcpy(stage, pre, pre_bytes);
+    char* tab = (char*)stage + skip;
     char* d = (char*)ctx->d_scratch + tab_off;
-    rc = upload(ctx, d, bytes4 + bytesc);
+    char* d_up = pre ? (char*)ctx->d_scratch : d;
+    if (tcp) {
+        tc_fill_addr(ctx, coef, k, rows, (unsigned long long*)tab);
+        rc = upload(ctx, d_up, skip + bytes);
+        if (rc)
+            return rc;
+        return tc_launch(ctx, tc_name, d_srcs, d_dsts, (const unsigned long long*)d, 0, k, rows, len,
+                         blocks, nullptr);
+    }
+    uint4* t4 = (uint4*)tab;
+    uint32_t* tc = (uint32_t*)(tab + n * sizeof(uint4));
+    fill_tables(coef, k, rows, rows_pad, t4, tc);
+    rc = upload(ctx, d_up, skip + bytes);
     if (rc)
         return rc;
     DotArgs a{};
     a.srcs = d_srcs;
     a.dsts = d_dsts;
     a.tabs4 = (const uint4*)d;
-    a.ctab = (const uint32_t*)(d + bytes4);
+    a.ctab = (const uint32_t*)(d + n * sizeof(uint4));
     a.tab_block_stride = 0;
     a.k = k;
     a.rows = rows;
@@ -262,19 +340,24 @@ int generic_from_host_coef(rsgpu_ctx* ctx, const uint8_t* coef, int k, int rows,
     a.len = len;
     a.blocks = blocks;
     a.status = nullptr;
-    a.bytewise = bytewise;
-    {
-        KTimer kt(ctx, "k_dot_generic", (size_t)blocks);
-        RS_HIP(ctx, launch_dot_generic(a, ctx->stream));
-    }
+    a.bytewise = !aligned;
+    KTimer kt(ctx, "k_dot_generic", (size_t)blocks);
+    RS_HIP(ctx, launch_dot_generic(a, ctx->stream));
     return RSGPU_OK;
+}
+
+// scratch bytes dot_from_host_coef needs for its table (either kernel)
+size_t dot_table_bytes(int k, int rows)
+{
+    return std::max(sizeof(unsigned long long) * (size_t)tc_table_elems(k, rows),
+                    (size_t)k * rows_pad_for(rows) * (sizeof(uint4) + sizeof(uint32_t)));
 }
 
 }  // namespace
 
 extern "C" {
 
-const char* rsgpu_version(void) { return "0.1.0"; }
+const char* rsgpu_version(void) { return "0.2.0"; }
 
 int rsgpu_create(int device, rsgpu_ctx** out)
 {
@@ -299,10 +382,6 @@ int rsgpu_destroy(rsgpu_ctx* ctx)
         return RSGPU_ERR_ARG;
     (void)hipSetDevice(ctx->device);
     (void)hipStreamSynchronize(ctx->stream);
-    if (ctx->aux) {
-        (void)hipStreamSynchronize(ctx->aux);
-        (void)hipStreamDestroy(ctx->aux);
-    }
     if (ctx->d_scratch)
         (void)hipFree(ctx->d_scratch);
     if (ctx->h_stage)
@@ -327,7 +406,15 @@ int rsgpu_set_stream(rsgpu_ctx* ctx, void* s)
 {
     if (!ctx)
         return RSGPU_ERR_ARG;
-    ctx->stream = (hipStream_t)s;
+    hipStream_t ns = (hipStream_t)s;
+    if (ns != ctx->stream) {
+        // everything enqueued on the old stream (kernels reading the scratch
+        // tables among them) is ordered before the new stream's work
+        hipEvent_t ev = sync_event(ctx);
+        RS_HIP(ctx, hipEventRecord(ev, ctx->stream));
+        RS_HIP(ctx, hipStreamWaitEvent(ns, ev, 0));
+    }
+    ctx->stream = ns;
     return RSGPU_OK;
 }
 
@@ -356,12 +443,11 @@ int rsgpu_timing_read(rsgpu_ctx* ctx, const char** names, float* ms, size_t* blo
     if (!ctx || max < 0)
         return RSGPU_ERR_ARG;
     RS_HIP(ctx, hipStreamSynchronize(ctx->stream));
-    if (ctx->aux)
-        RS_HIP(ctx, hipStreamSynchronize(ctx->aux));
     int n = 0;
     for (auto& r : ctx->recs) {
         if (n < max) {
             float t = 0;
+            (void)hipEventSynchronize(r.b);  // recorded on an earlier stream, possibly
             (void)hipEventElapsedTime(&t, r.a, r.b);
             if (names)
                 names[n] = r.name;
@@ -525,57 +611,19 @@ int rsgpu_ec_encode_data(rsgpu_ctx* ctx, int len, int k, int rows, const unsigne
     for (int r = 0; r < rows; ++r)
         aligned &= ((uintptr_t)coding[r] & 15) == 0;
     const size_t ptr_bytes = align_up(sizeof(void*) * (size_t)(k + rows), 256);
-    const int rows_pad = rows_pad_for(rows);
-    const bool tcp = aligned && len % 32 == 0 && use_tc(ctx, rows);
-    const size_t tab_bytes = tcp ? tc_table_bytes(k, rows)
-                                 : (size_t)k * rows_pad * (sizeof(uint4) + sizeof(uint32_t));
-    int rc = ensure_scratch(ctx, ptr_bytes + tab_bytes);
+    int rc = ensure_scratch(ctx, ptr_bytes + dot_table_bytes(k, rows));
     if (rc)
         return rc;
-    // pointer tables go through the same staging buffer after the tables:
-    // stage layout [ptrs | tables] keeps one upload per call
-    void* stage;
-    rc = get_stage(ctx, ptr_bytes + tab_bytes, &stage);
-    if (rc)
-        return rc;
-    void** hp = (void**)stage;
+    // the row pointers go up in the same upload as the coefficient table
+    std::vector<void*> hp((size_t)(k + rows));
     for (int j = 0; j < k; ++j)
         hp[j] = data[j];
     for (int r = 0; r < rows; ++r)
         hp[k + r] = coding[r];
-    if (tcp) {
-        // bit-sliced threaded-code kernel (rs_tc.hip): any coefficient matrix
-        tc_fill_addr(ctx, coef.data(), k, rows, (unsigned long long*)((char*)stage + ptr_bytes));
-        rc = upload(ctx, ctx->d_scratch, ptr_bytes + tab_bytes);
-        if (rc)
-            return rc;
-        char* d = (char*)ctx->d_scratch;
-        return tc_launch_shared(ctx, (const unsigned long long*)(d + ptr_bytes), k, rows, len, 1,
-                                (const uint8_t* const*)d, (uint8_t* const*)(d + sizeof(void*) * k),
-                                "k_rs_tc(ec_encode_data)");
-    }
-    uint4* t4 = (uint4*)((char*)stage + ptr_bytes);
-    uint32_t* tc = (uint32_t*)((char*)t4 + (size_t)k * rows_pad * sizeof(uint4));
-    fill_tables(coef.data(), k, rows, rows_pad, t4, tc);
-    rc = upload(ctx, ctx->d_scratch, ptr_bytes + tab_bytes);
-    if (rc)
-        return rc;
     char* d = (char*)ctx->d_scratch;
-    DotArgs a{};
-    a.srcs = (const uint8_t* const*)d;
-    a.dsts = (uint8_t* const*)(d + sizeof(void*) * k);
-    a.tabs4 = (const uint4*)(d + ptr_bytes);
-    a.ctab = (const uint32_t*)(d + ptr_bytes + (size_t)k * rows_pad * sizeof(uint4));
-    a.tab_block_stride = 0;
-    a.k = k;
-    a.rows = rows;
-    a.rows_pad = rows_pad;
-    a.len = len;
-    a.blocks = 1;
-    a.status = nullptr;
-    a.bytewise = !aligned;
-    RS_HIP(ctx, launch_dot_generic(a, ctx->stream));
-    return RSGPU_OK;
+    return dot_from_host_coef(ctx, coef.data(), k, rows, len, 1, (const uint8_t* const*)d,
+                              (uint8_t* const*)(d + sizeof(void*) * k), ptr_bytes, aligned,
+                              "k_rs_tc(ec_encode_data)", hp.data(), sizeof(void*) * hp.size());
 }
 
 int rsgpu_ec_encode_data_update(rsgpu_ctx* ctx, int len, int k, int rows, int vec_i,
@@ -644,8 +692,8 @@ int rsgpu_encode_blocks(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch, 
     // bit-sliced (len % 32 == 0) or nibble-table (len % 4 == 0).
     if (!coef && aligned && len % 32 == 0 && rs_bitsliced_available(k, e)) {
         KTimer kt(ctx, "k_rs_bs(encode)", blocks);
-        RS_HIP(ctx, launch_rs_bitsliced(k, e, d_src, nullptr, d_parity, (long long)pitch,
-                                        (long long)len, (long long)blocks, nullptr, ctx->stream));
+        RS_HIP(ctx, launch_rs_bitsliced(k, e, d_src, d_parity, (long long)pitch, (long long)len,
+                                        (long long)blocks, ctx->stream));
         return RSGPU_OK;
     }
     if (!coef && aligned && len % 4 == 0 && rs_encode_specialized_available(k, e)) {
@@ -664,10 +712,7 @@ int rsgpu_encode_blocks(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch, 
     }
     const size_t src_ptr_bytes = align_up(sizeof(void*) * (size_t)k * blocks, 256);
     const size_t dst_ptr_bytes = align_up(sizeof(void*) * (size_t)e * blocks, 256);
-    const int rows_pad = rows_pad_for(e);
-    const size_t tab_bytes = std::max((size_t)k * rows_pad * (sizeof(uint4) + sizeof(uint32_t)),
-                                      tc_table_bytes(k, e));
-    rc = ensure_scratch(ctx, src_ptr_bytes + dst_ptr_bytes + tab_bytes);
+    rc = ensure_scratch(ctx, src_ptr_bytes + dst_ptr_bytes + dot_table_bytes(k, e));
     if (rc)
         return rc;
     char* d = (char*)ctx->d_scratch;
@@ -675,218 +720,160 @@ int rsgpu_encode_blocks(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch, 
                                 (const uint8_t**)d, ctx->stream));
     RS_HIP(ctx, launch_row_ptrs(d_parity, (long long)pitch, e, (long long)blocks,
                                 (const uint8_t**)(d + src_ptr_bytes), ctx->stream));
-    if (aligned && len % 32 == 0 && use_tc(ctx, e))
-        return tc_from_host_coef(ctx, c.data(), k, e, (long long)len, (long long)blocks,
-                                 (const uint8_t* const*)d, (uint8_t* const*)(d + src_ptr_bytes),
-                                 src_ptr_bytes + dst_ptr_bytes, "k_rs_tc(encode)");
-    return generic_from_host_coef(ctx, c.data(), k, e, (long long)len, (long long)blocks,
-                                  (const uint8_t* const*)d, (uint8_t* const*)(d + src_ptr_bytes),
-                                  src_ptr_bytes + dst_ptr_bytes, !aligned);
+    return dot_from_host_coef(ctx, c.data(), k, e, (long long)len, (long long)blocks,
+                              (const uint8_t* const*)d, (uint8_t* const*)(d + src_ptr_bytes),
+                              src_ptr_bytes + dst_ptr_bytes, aligned, "k_rs_tc(encode)");
 }
 
-// Locate the handler table of k_rs_tc once per context: the query kernel
-// reports the table's first and end addresses; the layout must be exactly
-// tc_handler_count() handlers of tc_handler_stride() bytes, otherwise the
-// threaded-code path stays off (and k_dot_generic solves).  The address
-// table has 2048 entries: [slot][coefficient], each the handler copy that
-// serves the slot (tc_slot_copy).
-static int tc_init(rsgpu_ctx* ctx)
+int rsgpu_set_decode_kernel(rsgpu_ctx* ctx, int kernel)
 {
-    if (ctx->tc_state != 0)
-        return ctx->tc_state;
-    ctx->tc_state = -1;
-    unsigned long long* d = nullptr;
-    if (hipMalloc((void**)&d, 2050 * sizeof(unsigned long long)) != hipSuccess)
-        return -1;
-    unsigned long long se[2] = {0, 0};
-    if (tc_query_handlers(d + 2048, ctx->stream) != hipSuccess ||
-        hipMemcpyAsync(se, d + 2048, sizeof se, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
-        hipStreamSynchronize(ctx->stream) != hipSuccess) {
-        (void)hipFree(d);
-        return -1;
-    }
-    const unsigned long long stride = (unsigned long long)tc_handler_stride();
-    const unsigned long long count = (unsigned long long)tc_handler_count();
-    if (se[0] == 0 || se[1] - se[0] != count * stride || count % 256 != 0 || count > 2048) {
-        std::fprintf(stderr, "rsgpu: threaded-code handler table has an unexpected layout "
-                             "(%#llx..%#llx); using k_dot_generic\n", se[0], se[1]);
-        (void)hipFree(d);
-        return -1;
-    }
-    unsigned long long h[2048];
-    for (int s = 0; s < 8; ++s)
-        for (int c = 0; c < 256; ++c)
-            h[s * 256 + c] = se[0] + (unsigned long long)(tc_slot_copy(s) * 256 + c) * stride;
-    if (hipMemcpy(d, h, sizeof h, hipMemcpyHostToDevice) != hipSuccess) {
-        (void)hipFree(d);
-        return -1;
-    }
-    std::memcpy(ctx->h_tc_table, h, sizeof h);
-    ctx->d_tc_table = d;
-    ctx->tc_state = 1;
-    return 1;
-}
-
-namespace {
-
-size_t tc_table_bytes(int k, int rows)
-{
-    return sizeof(unsigned long long) * (size_t)k * tc_rows_per_pass(rows);
-}
-
-void tc_fill_addr(const rsgpu_ctx* ctx, const uint8_t* coef, int k, int rows, unsigned long long* h)
-{
-    const int slots = tc_rows_per_pass(rows);
-    for (int j = 0; j < k; ++j)
-        for (int s = 0; s < slots; ++s)
-            h[(size_t)j * slots + s] = ctx->h_tc_table[(s & 7) * 256 + (s < rows ? coef[(size_t)s * k + j] : 0)];
-}
-
-int tc_launch_shared(rsgpu_ctx* ctx, const unsigned long long* d_addr, int k, int rows, long long len,
-                     long long blocks, const uint8_t* const* d_srcs, uint8_t* const* d_dsts,
-                     const char* timer_name)
-{
-    TcArgs t{};
-    t.srcs = d_srcs;
-    t.dsts = d_dsts;
-    t.addr = d_addr;
-    t.addr_stride = 0;
-    t.k = k;
-    t.rows = rows;
-    t.len = len;
-    t.status = nullptr;
-    KTimer kt(ctx, timer_name, (size_t)blocks);
-    RS_HIP(ctx, launch_rs_tc(t, blocks, ctx->stream));
+    if (!ctx || kernel < RSGPU_DECODE_AUTO || kernel > RSGPU_DECODE_GENERAL)
+        return fail(ctx, RSGPU_ERR_ARG, "rsgpu_set_decode_kernel: unknown kernel");
+    ctx->decode_kernel = kernel;
     return RSGPU_OK;
 }
 
-int tc_from_host_coef(rsgpu_ctx* ctx, const uint8_t* coef, int k, int rows, long long len,
-                      long long blocks, const uint8_t* const* d_srcs, uint8_t* const* d_dsts,
-                      size_t tab_off, const char* timer_name)
+}  // extern "C"
+
+namespace {
+
+// How rsgpu_decode_blocks runs for a geometry (prepare and apply agree as
+// long as the context's decode kernel setting does not change in between).
+enum class Plan {
+    one_matrix,  // k_decode_prepare_syn (closed form) + k_rs_tc
+    fused,       // k_decode_prepare_syn (e x e) + k_rs_decode_fused
+    general_tc,  // k_decode_prepare (k x k inversion) + k_rs_tc passes
+    general_dot  // k_decode_prepare + k_dot_generic (unaligned / odd lengths)
+};
+
+bool rows_aligned(size_t len, size_t pitch, const void* a, const void* b, const void* c)
 {
-    const size_t bytes = tc_table_bytes(k, rows);
-    void* stage;
-    int rc = get_stage(ctx, bytes, &stage);
-    if (rc)
-        return rc;
-    tc_fill_addr(ctx, coef, k, rows, (unsigned long long*)stage);
-    char* d = (char*)ctx->d_scratch + tab_off;
-    rc = upload(ctx, d, bytes);
-    if (rc)
-        return rc;
-    return tc_launch_shared(ctx, (const unsigned long long*)d, k, rows, len, blocks, d_srcs, d_dsts,
-                            timer_name);
+    return len % 32 == 0 && pitch % 16 == 0 && (uintptr_t)a % 16 == 0 && (uintptr_t)b % 16 == 0 &&
+           (uintptr_t)c % 16 == 0;
+}
+
+Plan decode_plan(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch, const void* src,
+                 const void* par, const void* out)
+{
+    if (!rows_aligned(len, pitch, src, par, out) || !tc_ready(ctx))
+        return Plan::general_dot;
+    const int want = ctx->decode_kernel;
+    if (want == RSGPU_DECODE_GENERAL || e > 32)
+        return Plan::general_tc;
+    // the fused kernel measured 3 % faster at (k 100, e 20) only
+    if (rs_decode_fused_available(k, e) &&
+        (want == RSGPU_DECODE_FUSED || (want == RSGPU_DECODE_AUTO && k == 100 && e == 20)))
+        return Plan::fused;
+    return Plan::one_matrix;
+}
+
+// Workspace: [emask B x 16 B | survivor ptrs B x k | output ptrs B x e |
+// coefficient region], the region sized for the largest consumer: k_rs_tc
+// handler addresses (pass layout; the fused kernel's e x e + (k-e) x e
+// tables are no larger) or the v_perm tables.
+struct WsLayout {
+    size_t surv, outp, tab, tab2, total;
+};
+
+WsLayout ws_layout(int k, int e, size_t blocks)
+{
+    WsLayout w{};
+    size_t o = align_up(16 * blocks, 256);
+    w.surv = o;
+    o = align_up(o + sizeof(void*) * (size_t)k * blocks, 256);
+    w.outp = o;
+    o = align_up(o + sizeof(void*) * (size_t)e * blocks, 256);
+    w.tab = o;
+    // fused: syndrome-phase addresses after the e x e ones
+    w.tab2 = align_up(o + sizeof(unsigned long long) * (size_t)e * tc_rows_per_pass(e) * blocks, 256);
+    const size_t tc_bytes = sizeof(unsigned long long) * (size_t)tc_table_elems(k, e) * blocks;
+    const size_t fused_bytes = (w.tab2 - o) + sizeof(unsigned long long) * (size_t)(k > e ? k - e : 0) *
+                                                  tc_rows_per_pass(e) * blocks;
+    const size_t dot_bytes = (sizeof(uint4) + sizeof(uint32_t)) * (size_t)k * rows_pad_for(e) * blocks;
+    w.total = align_up(o + std::max({tc_bytes, fused_bytes, dot_bytes}), 256);
+    return w;
+}
+
+// k_decode_prepare launch for the general plans (enc: device m x k matrix
+// or nullptr for gf_gen_rs_matrix)
+int general_prepare(rsgpu_ctx* ctx, Plan plan, int k, int m, int nerrs, bool originals_only,
+                    size_t pitch, size_t blocks, const uint8_t* enc, const unsigned char* d_src,
+                    const unsigned char* d_parity, const unsigned char* d_err, unsigned char* d_out,
+                    void* d_workspace, int* d_status)
+{
+    const WsLayout w = ws_layout(k, nerrs, blocks);
+    char* ws = (char*)d_workspace;
+    PrepArgs p{};
+    p.k = k;
+    p.m = m;
+    p.nerrs = nerrs;
+    p.rows_pad = rows_pad_for(nerrs);
+    p.blocks = (long long)blocks;
+    p.err = d_err;
+    p.enc = enc;
+    p.originals_only = originals_only ? 1 : 0;
+    p.src = d_src;
+    p.src_pitch = (long long)pitch;
+    p.par = d_parity;
+    p.par_pitch = (long long)pitch;
+    p.out = d_out;
+    p.out_pitch = (long long)pitch;
+    p.surv_ptrs = (const uint8_t**)(ws + w.surv);
+    p.out_ptrs = (uint8_t**)(ws + w.outp);
+    p.status = d_status;
+    if (plan == Plan::general_tc) {
+        p.tc_table = ctx->d_tc_table;
+        p.tc_addr = (unsigned long long*)(ws + w.tab);
+        p.tc_block_stride = tc_table_elems(k, nerrs);
+    } else {
+        p.tabs4 = (uint4*)(ws + w.tab);
+        p.ctab = (uint32_t*)(ws + w.tab + sizeof(uint4) * (size_t)k * p.rows_pad * blocks);
+        p.tab_block_stride = (long long)k * p.rows_pad;
+    }
+    KTimer kt(ctx, "k_decode_prepare", blocks);
+    RS_HIP(ctx, launch_decode_prepare(p, ctx->stream));
+    return RSGPU_OK;
+}
+
+int general_apply(rsgpu_ctx* ctx, Plan plan, int k, int nerrs, size_t len, size_t pitch,
+                  size_t blocks, bool aligned, void* d_workspace, const int* d_status)
+{
+    const WsLayout w = ws_layout(k, nerrs, blocks);
+    char* ws = (char*)d_workspace;
+    if (plan == Plan::general_tc)
+        return tc_launch(ctx, "k_rs_tc(decode)", (const uint8_t* const*)(ws + w.surv),
+                         (uint8_t* const*)(ws + w.outp), (const unsigned long long*)(ws + w.tab),
+                         tc_table_elems(k, nerrs), k, nerrs, (long long)len, (long long)blocks,
+                         d_status);
+    const int rows_pad = rows_pad_for(nerrs);
+    DotArgs a{};
+    a.srcs = (const uint8_t* const*)(ws + w.surv);
+    a.dsts = (uint8_t* const*)(ws + w.outp);
+    a.tabs4 = (const uint4*)(ws + w.tab);
+    a.ctab = (const uint32_t*)(ws + w.tab + sizeof(uint4) * (size_t)k * rows_pad * blocks);
+    a.tab_block_stride = (long long)k * rows_pad;
+    a.k = k;
+    a.rows = nerrs;
+    a.rows_pad = rows_pad;
+    a.len = (long long)len;
+    a.blocks = (long long)blocks;
+    a.status = d_status;
+    a.bytewise = !aligned;
+    (void)pitch;
+    KTimer kt(ctx, "k_dot_generic(decode)", blocks);
+    RS_HIP(ctx, launch_dot_generic(a, ctx->stream));
+    return RSGPU_OK;
 }
 
 }  // namespace
 
-// The threaded-code solve serves e <= 32 on the syndrome path.  Decided once
-// per context (RSGPU_NO_TC=1 at first use selects k_dot_generic instead, for
-// comparison), so prepare and apply always agree on the workspace contents.
-static bool use_tc(rsgpu_ctx* ctx, int e)
-{
-    if (e > 32)
-        return false;
-    if (ctx->tc_state == 0) {
-        const char* v = std::getenv("RSGPU_NO_TC");
-        if (v && v[0] == '1')
-            ctx->tc_state = -1;
-    }
-    return tc_init(ctx) == 1;
-}
-
-// Decode kernels of the syndrome path once threaded code is available
-// (RSGPU_DECODE, read once per process):
-//   direct (default)  one matrix: k_rs_tc over the k - e survivors and the e
-//                     parity rows with the e x k decode rows (one pass, HBM
-//                     traffic (k + e) L per block)
-//   fused             k_rs_decode_fused: syndromes + e x e solve per tile
-//                     (the default for k 100, e 20, where it measured faster)
-//                     (instantiated codes only)
-//   split             k_rs_bs syndromes to HBM, then the in-place k_rs_tc solve
-// RSGPU_NO_FUSED=1 (older switch) means split.
-enum class DecodeMode { direct, fused, split };
-
-static DecodeMode decode_mode(int k, int e)
-{
-    // -1: no override, per-code default below
-    static const int forced = [] {
-        const char* v = std::getenv("RSGPU_DECODE");
-        const char* nf = std::getenv("RSGPU_NO_FUSED");
-        if (v && std::strcmp(v, "fused") == 0)
-            return (int)DecodeMode::fused;
-        if ((v && std::strcmp(v, "split") == 0) || (nf && nf[0] == '1'))
-            return (int)DecodeMode::split;
-        if (v && std::strcmp(v, "direct") == 0)
-            return (int)DecodeMode::direct;
-        return -1;
-    }();
-    DecodeMode m = DecodeMode::direct;
-    if (forced >= 0)
-        m = (DecodeMode)forced;
-    else if (k == 100 && e == 20)
-        m = DecodeMode::fused;  // measured 2 % faster there (BASELINE C5)
-    if (m == DecodeMode::fused && !rs_decode_fused_available(k, e))
-        return DecodeMode::split;
-    return m;
-}
-
-static bool use_fused(rsgpu_ctx*, int k, int e) { return decode_mode(k, e) == DecodeMode::fused; }
-static bool use_direct(rsgpu_ctx*, int k, int e) { return decode_mode(k, e) == DecodeMode::direct; }
-
-// Syndrome decode (bit-sliced syndromes + runtime e x e in place) applies to
-// the instantiated codes with 32-byte-multiple rows; otherwise the direct
-// k x k inversion + e x k dot product.
-static bool use_syn_path(int k, int e, size_t len, size_t pitch, const void* src, const void* par,
-                         const void* out)
-{
-    return rs_bitsliced_available(k, e) && len % 32 == 0 && pitch % 16 == 0 &&
-           (uintptr_t)src % 16 == 0 && (uintptr_t)par % 16 == 0 && (uintptr_t)out % 16 == 0;
-}
-
-// General decode (k x k inversion) through k_rs_tc: e <= 32 with 32-byte
-// multiple, 16-byte aligned rows (RSGPU_NO_TC=1 keeps k_dot_generic).
-static bool use_tc_general(rsgpu_ctx* ctx, int e, size_t len, size_t pitch, const void* src,
-                           const void* par, const void* out)
-{
-    return len % 32 == 0 && pitch % 16 == 0 && (uintptr_t)src % 16 == 0 && (uintptr_t)par % 16 == 0 &&
-           (uintptr_t)out % 16 == 0 && use_tc(ctx, e);
-}
-
-static void decode_ws_layout(int k, int e, size_t blocks, size_t* off_surv, size_t* off_out,
-                             size_t* off_t4, size_t* off_tc, size_t* off_tca, size_t* off_sa,
-                             size_t* total)
-{
-    const int rows_pad = rows_pad_for(e);
-    size_t o = 16 * blocks;  // emask [blocks][2] u64 at offset 0
-    o = align_up(o, 256);
-    *off_surv = o;
-    o = align_up(o + sizeof(void*) * (size_t)k * blocks, 256);
-    *off_out = o;
-    o = align_up(o + sizeof(void*) * (size_t)e * blocks, 256);
-    *off_t4 = o;
-    o = align_up(o + sizeof(uint4) * (size_t)k * rows_pad * blocks, 256);
-    *off_tc = o;
-    o = align_up(o + sizeof(uint32_t) * (size_t)k * rows_pad * blocks, 256);
-    // k_rs_tc handler addresses: [blocks][e][tc_rows] (split / fused solve)
-    // or, for the one-matrix decode, [blocks][k][tc_rows] spanning this
-    // region and the next one
-    *off_tca = o;
-    o = align_up(o + sizeof(unsigned long long) * (size_t)e * tc_rows_per_pass(e) * blocks, 256);
-    *off_sa = o;  // fused decode: syndrome-phase handler addresses [blocks][k-e][tc_rows]
-    o = align_up(o + sizeof(unsigned long long) * (size_t)(k > e ? k - e : 0) * tc_rows_per_pass(e) *
-                         blocks,
-                 256);
-    *total = o;
-}
+extern "C" {
 
 size_t rsgpu_decode_workspace_bytes(int k, int e, size_t blocks)
 {
     if (k <= 0 || e <= 0)
         return 256;
-    size_t a, b, c, d, x, y, t;
-    decode_ws_layout(k, e, blocks, &a, &b, &c, &d, &x, &y, &t);
-    return t;
+    return ws_layout(k, e, blocks).total;
 }
 
 int rsgpu_decode_prepare(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch, size_t blocks,
@@ -901,55 +888,22 @@ int rsgpu_decode_prepare(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch,
         return RSGPU_OK;
     if (e > k || !d_err || !d_workspace || !d_status)
         return fail(ctx, RSGPU_ERR_ARG, "rsgpu_decode_prepare: bad arguments");
-    size_t o_surv, o_out, o_t4, o_tc, o_tca, o_sa, total;
-    decode_ws_layout(k, e, blocks, &o_surv, &o_out, &o_t4, &o_tc, &o_tca, &o_sa, &total);
-    char* ws = (char*)d_workspace;
-    const int rows_pad = rows_pad_for(e);
-    if (use_syn_path(k, e, len, pitch, d_src, d_parity, d_out)) {
-        const bool tcp = use_tc(ctx, e);
+    const Plan plan = decode_plan(ctx, k, e, len, pitch, d_src, d_parity, d_out);
+    if (plan == Plan::one_matrix || plan == Plan::fused) {
+        const WsLayout w = ws_layout(k, e, blocks);
+        char* ws = (char*)d_workspace;
+        const bool one = plan == Plan::one_matrix;
         KTimer kt(ctx, "k_decode_prepare_syn", blocks);
         RS_HIP(ctx, launch_decode_prepare_syn(
-                        k, e, rows_pad, (long long)blocks, d_err, d_out, (long long)pitch,
-                        (const uint8_t**)(ws + o_surv), (uint8_t**)(ws + o_out),
-                        tcp ? nullptr : (uint4*)(ws + o_t4), tcp ? nullptr : (uint32_t*)(ws + o_tc),
-                        (long long)e * rows_pad, tcp ? ctx->d_tc_table : nullptr,
-                        tcp ? (unsigned long long*)(ws + o_tca) : nullptr, tc_rows_per_pass(e),
-                        (unsigned long long*)ws, d_status,
-                        tcp && use_fused(ctx, k, e) ? (unsigned long long*)(ws + o_sa) : nullptr,
-                        d_src, d_parity,
-                        tcp && use_direct(ctx, k, e) ? (unsigned long long*)(ws + o_tca) : nullptr,
-                        ctx->stream));
+                        k, e, (long long)blocks, d_err, d_out, (long long)pitch,
+                        (const uint8_t**)(ws + w.surv), (uint8_t**)(ws + w.outp), ctx->d_tc_table,
+                        one ? nullptr : (unsigned long long*)(ws + w.tab), (unsigned long long*)ws,
+                        d_status, one ? nullptr : (unsigned long long*)(ws + w.tab2), d_src, d_parity,
+                        one ? (unsigned long long*)(ws + w.tab) : nullptr, ctx->stream));
         return RSGPU_OK;
     }
-    PrepArgs p{};
-    p.k = k;
-    p.e = e;
-    p.rows_pad = rows_pad;
-    p.blocks = (long long)blocks;
-    p.err = d_err;
-    p.src = d_src;
-    p.src_pitch = (long long)pitch;
-    p.par = d_parity;
-    p.par_pitch = (long long)pitch;
-    p.out = d_out;
-    p.out_pitch = (long long)pitch;
-    p.surv_ptrs = (const uint8_t**)(ws + o_surv);
-    p.out_ptrs = (uint8_t**)(ws + o_out);
-    p.tabs4 = (uint4*)(ws + o_t4);
-    p.ctab = (uint32_t*)(ws + o_tc);
-    p.tab_block_stride = (long long)k * rows_pad;
-    p.status = d_status;
-    if (use_tc_general(ctx, e, len, pitch, d_src, d_parity, d_out)) {
-        // [blocks][k][tc_rows] spans the tca and sa regions (k >= e)
-        p.tc_table = ctx->d_tc_table;
-        p.tc_addr = (unsigned long long*)(ws + o_tca);
-        p.tc_rows = tc_rows_per_pass(e);
-        p.tabs4 = nullptr;
-        p.ctab = nullptr;
-    }
-    KTimer kt(ctx, "k_decode_prepare", blocks);
-    RS_HIP(ctx, launch_decode_prepare(p, ctx->stream));
-    return RSGPU_OK;
+    return general_prepare(ctx, plan, k, k + e, e, true, pitch, blocks, nullptr, d_src, d_parity,
+                           d_err, d_out, d_workspace, d_status);
 }
 
 int rsgpu_decode_apply(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch, size_t blocks,
@@ -963,137 +917,28 @@ int rsgpu_decode_apply(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch, s
         return RSGPU_OK;
     if (e > k || !d_workspace || !d_status)
         return fail(ctx, RSGPU_ERR_ARG, "rsgpu_decode_apply: bad arguments");
-    size_t o_surv, o_out, o_t4, o_tc, o_tca, o_sa, total;
-    decode_ws_layout(k, e, blocks, &o_surv, &o_out, &o_t4, &o_tc, &o_tca, &o_sa, &total);
+    const Plan plan = decode_plan(ctx, k, e, len, pitch, d_src, d_parity, d_out);
+    const WsLayout w = ws_layout(k, e, blocks);
     char* ws = (char*)d_workspace;
-    const int rows_pad = rows_pad_for(e);
-    if (use_syn_path(k, e, len, pitch, d_src, d_parity, d_out)) {
-        // Syndromes into out (bit-sliced, memory-latency bound), then the
-        // in-place e x e solve (VALU bound; blocks with a bad status are
-        // skipped).  The blocks are cut into chunks and the two kernels run
-        // on two streams so that the syndromes of chunk i+1 overlap the solve
-        // of chunk i.
-        const bool tcp = use_tc(ctx, e);
-        if (tcp && use_direct(ctx, k, e)) {
-            // one pass, one matrix (prepared by k_decode_prepare_syn)
-            TcArgs t{};
-            t.srcs = (const uint8_t* const*)(ws + o_surv);
-            t.dsts = (uint8_t* const*)(ws + o_out);
-            t.addr = (const unsigned long long*)(ws + o_tca);
-            t.addr_stride = (long long)k * tc_rows_per_pass(e);
-            t.k = k;
-            t.rows = e;
-            t.len = (long long)len;
-            t.status = d_status;
-            KTimer kt(ctx, "k_rs_tc(decode)", blocks);
-            RS_HIP(ctx, launch_rs_tc(t, (long long)blocks, ctx->stream));
-            return RSGPU_OK;
-        }
-        if (tcp && use_fused(ctx, k, e)) {
-            // one pass: syndromes + solve per column tile (rs_decode_fused.hip)
-            KTimer kt(ctx, "k_rs_decode_fused", blocks);
-            RS_HIP(ctx, launch_rs_decode_fused(k, e, d_src, d_parity, d_out, (long long)pitch,
-                                               (long long)len, (long long)blocks,
-                                               (const uint64_t*)ws,
-                                               (const unsigned long long*)(ws + o_tca),
-                                               (const unsigned long long*)(ws + o_sa), d_status,
-                                               ctx->stream));
-            return RSGPU_OK;
-        }
-        const size_t chunks = decode_chunk_count(ctx, blocks);
-        hipStream_t solve_stream = ctx->stream;
-        if (chunks > 1) {
-            if (!ctx->aux)
-                RS_HIP(ctx, hipStreamCreateWithFlags(&ctx->aux, hipStreamNonBlocking));
-            solve_stream = ctx->aux;
-        }
-        const size_t per = (blocks + chunks - 1) / chunks;
-        const long long tstride = (long long)e * rows_pad;
-        for (size_t b0 = 0; b0 < blocks; b0 += per) {
-            const size_t nb = std::min(per, blocks - b0);
-            {
-                KTimer kt(ctx, "k_rs_bs(syndrome)", nb);
-                RS_HIP(ctx, launch_rs_bitsliced(k, e, d_src + b0 * k * pitch, d_parity + b0 * e * pitch,
-                                                d_out + b0 * e * pitch, (long long)pitch,
-                                                (long long)len, (long long)nb,
-                                                (const uint64_t*)ws + 2 * b0, ctx->stream));
-            }
-            if (chunks > 1) {
-                hipEvent_t ev = sync_event(ctx);
-                RS_HIP(ctx, hipEventRecord(ev, ctx->stream));
-                RS_HIP(ctx, hipStreamWaitEvent(solve_stream, ev, 0));
-            }
-            if (tcp) {
-                TcArgs t{};
-                t.srcs = (const uint8_t* const*)(ws + o_surv) + b0 * e;
-                t.dsts = (uint8_t* const*)(ws + o_out) + b0 * e;
-                t.addr = (const unsigned long long*)(ws + o_tca) + b0 * e * tc_rows_per_pass(e);
-                t.addr_stride = (long long)e * tc_rows_per_pass(e);
-                t.k = e;
-                t.rows = e;
-                t.len = (long long)len;
-                t.status = d_status + b0;
-                KTimer kt(ctx, "k_rs_tc(solve)", nb, solve_stream);
-                RS_HIP(ctx, launch_rs_tc(t, (long long)nb, solve_stream));
-                continue;
-            }
-            DotArgs a{};
-            a.srcs = (const uint8_t* const*)(ws + o_surv) + b0 * e;
-            a.dsts = (uint8_t* const*)(ws + o_out) + b0 * e;
-            a.tabs4 = (const uint4*)(ws + o_t4) + b0 * tstride;
-            a.ctab = (const uint32_t*)(ws + o_tc) + b0 * tstride;
-            a.tab_block_stride = tstride;
-            a.k = e;
-            a.rows = e;
-            a.rows_pad = rows_pad;
-            a.len = (long long)len;
-            a.blocks = (long long)nb;
-            a.status = d_status + b0;
-            a.bytewise = false;
-            KTimer kt(ctx, "k_dot_generic(solve)", nb, solve_stream);
-            RS_HIP(ctx, launch_dot_generic(a, solve_stream));
-        }
-        if (chunks > 1) {
-            hipEvent_t ev = sync_event(ctx);
-            RS_HIP(ctx, hipEventRecord(ev, solve_stream));
-            RS_HIP(ctx, hipStreamWaitEvent(ctx->stream, ev, 0));
-        }
-        return RSGPU_OK;
-    }
-    if (use_tc_general(ctx, e, len, pitch, d_src, d_parity, d_out)) {
-        // any geometry, e <= 32, 32-byte-multiple aligned rows: the rows of
-        // inv(b) through the threaded-code kernel (prepared by k_decode_prepare)
-        TcArgs t{};
-        t.srcs = (const uint8_t* const*)(ws + o_surv);
-        t.dsts = (uint8_t* const*)(ws + o_out);
-        t.addr = (const unsigned long long*)(ws + o_tca);
-        t.addr_stride = (long long)k * tc_rows_per_pass(e);
-        t.k = k;
-        t.rows = e;
-        t.len = (long long)len;
-        t.status = d_status;
-        KTimer kt(ctx, "k_rs_tc(decode)", blocks);
-        RS_HIP(ctx, launch_rs_tc(t, (long long)blocks, ctx->stream));
+    if (plan == Plan::one_matrix)
+        // one pass, one matrix over the k - e survivors and the e parity rows
+        return tc_launch(ctx, "k_rs_tc(decode)", (const uint8_t* const*)(ws + w.surv),
+                         (uint8_t* const*)(ws + w.outp), (const unsigned long long*)(ws + w.tab),
+                         (long long)k * tc_rows_per_pass(e), k, e, (long long)len,
+                         (long long)blocks, d_status);
+    if (plan == Plan::fused) {
+        // one pass: syndromes + solve per column tile (rs_decode_fused.hip)
+        KTimer kt(ctx, "k_rs_decode_fused", blocks);
+        RS_HIP(ctx, launch_rs_decode_fused(k, e, d_src, d_parity, d_out, (long long)pitch,
+                                           (long long)len, (long long)blocks, (const uint64_t*)ws,
+                                           (const unsigned long long*)(ws + w.tab),
+                                           (const unsigned long long*)(ws + w.tab2), d_status,
+                                           ctx->stream));
         return RSGPU_OK;
     }
     const bool aligned = ((uintptr_t)d_src % 16 == 0) && ((uintptr_t)d_parity % 16 == 0) &&
                          ((uintptr_t)d_out % 16 == 0) && (pitch % 16 == 0);
-    DotArgs a{};
-    a.srcs = (const uint8_t* const*)(ws + o_surv);
-    a.dsts = (uint8_t* const*)(ws + o_out);
-    a.tabs4 = (const uint4*)(ws + o_t4);
-    a.ctab = (const uint32_t*)(ws + o_tc);
-    a.tab_block_stride = (long long)k * rows_pad;
-    a.k = k;
-    a.rows = e;
-    a.rows_pad = rows_pad;
-    a.len = (long long)len;
-    a.blocks = (long long)blocks;
-    a.status = d_status;
-    a.bytewise = !aligned;
-    KTimer kt(ctx, "k_dot_generic(decode)", blocks);
-    RS_HIP(ctx, launch_dot_generic(a, ctx->stream));
-    return RSGPU_OK;
+    return general_apply(ctx, plan, k, e, len, pitch, blocks, aligned, d_workspace, d_status);
 }
 
 int rsgpu_decode_blocks(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch, size_t blocks,
@@ -1107,6 +952,54 @@ int rsgpu_decode_blocks(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch, 
         return rc;
     return rsgpu_decode_apply(ctx, k, e, len, pitch, blocks, d_src, d_parity, d_out, d_workspace,
                               d_status);
+}
+
+size_t rsgpu_decode_general_workspace_bytes(int k, int m, int nerrs, size_t blocks)
+{
+    if (k <= 0 || m < k || nerrs <= 0)
+        return 256;
+    return ws_layout(k, nerrs, blocks).total;
+}
+
+int rsgpu_decode_general(rsgpu_ctx* ctx, int k, int m, size_t len, size_t pitch, size_t blocks,
+                         const unsigned char* encode_matrix, const unsigned char* d_src,
+                         const unsigned char* d_parity, const unsigned char* d_err, int nerrs,
+                         unsigned char* d_out, void* d_workspace, int* d_status)
+{
+    int rc = check_geom(ctx, k, m - k, len, pitch, blocks);
+    if (rc)
+        return rc;
+    if (nerrs < 0 || nerrs > m - k)
+        return fail(ctx, RSGPU_ERR_ARG, "rsgpu_decode_general: nerrs must be in [0, m - k]");
+    if (nerrs == 0)
+        return RSGPU_OK;
+    if (!d_err || !d_workspace || !d_status || !d_out)
+        return fail(ctx, RSGPU_ERR_ARG, "rsgpu_decode_general: bad arguments");
+    const bool tcp = rows_aligned(len, pitch, d_src, d_parity, d_out) && tc_ready(ctx);
+    const Plan plan = tcp ? Plan::general_tc : Plan::general_dot;
+    const uint8_t* d_enc = nullptr;
+    if (encode_matrix) {
+        const size_t bytes = (size_t)m * k;
+        rc = ensure_scratch(ctx, bytes);
+        if (rc)
+            return rc;
+        void* stage;
+        rc = get_stage(ctx, bytes, &stage);
+        if (rc)
+            return rc;
+        std::memcpy(stage, encode_matrix, bytes);
+        rc = upload(ctx, ctx->d_scratch, bytes);
+        if (rc)
+            return rc;
+        d_enc = (const uint8_t*)ctx->d_scratch;
+    }
+    rc = general_prepare(ctx, plan, k, m, nerrs, false, pitch, blocks, d_enc, d_src, d_parity, d_err,
+                         d_out, d_workspace, d_status);
+    if (rc || len == 0)
+        return rc;
+    const bool aligned = ((uintptr_t)d_src % 16 == 0) && ((uintptr_t)d_parity % 16 == 0) &&
+                         ((uintptr_t)d_out % 16 == 0) && (pitch % 16 == 0);
+    return general_apply(ctx, plan, k, nerrs, len, pitch, blocks, aligned, d_workspace, d_status);
 }
 
 int rsgpu_verify_blocks(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch, size_t blocks,

@@ -121,6 +121,7 @@ struct gpu_decoder {
         m_s->check(rsgpu_malloc(m_s->ctx, (void**)&status, sizeof(int) * B), "alloc status");
         m_s->check(rsgpu_malloc(m_s->ctx, (void**)&mism, sizeof(unsigned long long) * B), "alloc");
         m_s->check(rsgpu_memcpy_h2d(m_s->ctx, err, h_err.data(), h_err.size()), "upload err");
+        h_list = h_err;
         h_status.assign(B, -1);
     }
     // Drop-in form of isa_decoder(symbols, symbol_size, erased_symbols)
@@ -138,17 +139,35 @@ struct gpu_decoder {
         rsgpu_free(m_s->ctx, status);
         rsgpu_free(m_s->ctx, mism);
     }
-    // isa.cpp:169-213
+    // isa.cpp:169-213.  The synchronous (reference-shaped) decoder knows the
+    // outcome on return: 0 when a block's matrix was singular or its
+    // erasure list malformed, as decode_all returns 0 on "BAD MATRIX"
+    // (isa.cpp:185-190).  Batched decoders return the payload count and
+    // report failures through is_complete() after finish().
     uint32_t decode_all(const std::shared_ptr<gpu_encoder>& enc)
     {
         m_s->check(rsgpu_decode_blocks(m_s->ctx, (int)k, (int)e, L, pitch, B, enc->src, enc->par,
                                        err, out, ws, status),
                    "rsgpu_decode_blocks");
         m_decoded = true;
-        if (synchronous)
+        if (synchronous) {
             finish();
+            if (!is_complete())
+                return 0;
+        }
         return enc->payload_count();
     }
+    // Replace the erasure lists ([blocks][e], ascending originals) drawn by
+    // the constructor, e.g. with a malformed list to exercise the failure
+    // path (test hook; the reference draws them in its constructor only).
+    void set_erasures(const std::vector<unsigned char>& h_err)
+    {
+        if (h_err.size() != (size_t)B * e)
+            throw std::runtime_error("set_erasures: want blocks x erased entries");
+        m_s->check(rsgpu_memcpy_h2d(m_s->ctx, err, h_err.data(), h_err.size()), "upload err");
+        h_list = h_err;
+    }
+    const std::vector<unsigned char>& erasures() const { return h_list; }
     void finish()
     {
         m_s->check(rsgpu_memcpy_d2h(m_s->ctx, h_status.data(), status, sizeof(int) * B), "status");
@@ -190,6 +209,7 @@ struct gpu_decoder {
     int* status = nullptr;
     unsigned long long* mism = nullptr;
     std::vector<int> h_status;
+    std::vector<unsigned char> h_list;  // erasure lists [blocks][e] (host copy)
     bool m_decoded = false;
     bool synchronous = false;
 };

@@ -45,6 +45,8 @@ RSGPU_OK = 0
 ERRORS = {-1: "RSGPU_ERR_ARG", -2: "RSGPU_ERR_HIP", -3: "RSGPU_ERR_SINGULAR",
           -4: "RSGPU_ERR_NOMEM", -5: "RSGPU_ERR_UNSUPPORTED"}
 MAX_SOURCES = 250  # TEST_SOURCES, isa.cpp:25-27
+# rsgpu_set_decode_kernel choices (include/rsgpu.h)
+DECODE_KERNELS = {"auto": 0, "one_matrix": 1, "fused": 2, "general": 3}
 
 vp = C.c_void_p
 sz = C.c_size_t
@@ -78,6 +80,10 @@ _SIGS = {
                                               C.POINTER(vp)]),
     "rsgpu_encode_blocks": (C.c_int, [vp, C.c_int, C.c_int, sz, sz, sz, vp, vp, vp]),
     "rsgpu_decode_workspace_bytes": (sz, [C.c_int, C.c_int, sz]),
+    "rsgpu_set_decode_kernel": (C.c_int, [vp, C.c_int]),
+    "rsgpu_decode_general_workspace_bytes": (sz, [C.c_int, C.c_int, C.c_int, sz]),
+    "rsgpu_decode_general": (C.c_int, [vp, C.c_int, C.c_int, sz, sz, sz, vp, vp, vp, vp, C.c_int,
+                                       vp, vp, vp]),
     "rsgpu_decode_blocks": (C.c_int, [vp, C.c_int, C.c_int, sz, sz, sz, vp, vp, vp, vp, vp, vp]),
     "rsgpu_decode_prepare": (C.c_int, [vp, C.c_int, C.c_int, sz, sz, sz, vp, vp, vp, vp, vp,
                                        vp]),
@@ -215,9 +221,18 @@ class Context:
     def set_stream(self, stream: int) -> None:
         self.check(lib().rsgpu_set_stream(self._h, stream), "rsgpu_set_stream")
 
+    def get_stream(self) -> int:
+        return lib().rsgpu_get_stream(self._h) or 0
+
     def set_torch_stream(self) -> None:
         import torch
         self.set_stream(torch.cuda.current_stream().cuda_stream)
+
+    def set_decode_kernel(self, kernel: str) -> None:
+        """Decode kernel of decode_blocks: auto | one_matrix | fused | general
+        (include/rsgpu.h rsgpu_set_decode_kernel)."""
+        self.check(lib().rsgpu_set_decode_kernel(self._h, DECODE_KERNELS[kernel]),
+                   "rsgpu_set_decode_kernel")
 
     def timing_enable(self, on: bool = True) -> None:
         self.check(lib().rsgpu_timing_enable(self._h, 1 if on else 0), "rsgpu_timing_enable")
@@ -279,6 +294,19 @@ class Context:
                                             _ptr(d_par), _ptr(d_out), _ptr(d_ws), _ptr(d_status)),
                    "rsgpu_decode_apply")
 
+    def decode_general(self, k, m, length, pitch, blocks, encode_matrix, d_src, d_par, d_err, nerrs,
+                       d_out, d_ws, d_status) -> None:
+        """gf_gen_decode_matrix + recovery (erasure_code_base_test.c:133-213)
+        for any m x k encode matrix (None: gf_gen_rs_matrix) and erasures
+        among data and parity rows."""
+        mp = None
+        if encode_matrix is not None:
+            encode_matrix = np.ascontiguousarray(encode_matrix, np.uint8).reshape(m, k)
+            mp = encode_matrix.ctypes.data
+        self.check(lib().rsgpu_decode_general(self._h, k, m, length, pitch, blocks, mp, _ptr(d_src),
+                                              _ptr(d_par), _ptr(d_err), nerrs, _ptr(d_out),
+                                              _ptr(d_ws), _ptr(d_status)), "rsgpu_decode_general")
+
     def verify_blocks(self, k, e, length, pitch, blocks, d_src, d_out, d_err, d_mism) -> None:
         self.check(lib().rsgpu_verify_blocks(self._h, k, e, length, pitch, blocks, _ptr(d_src),
                                              _ptr(d_out), _ptr(d_err), _ptr(d_mism)),
@@ -291,6 +319,10 @@ class Context:
 
 def decode_workspace_bytes(k: int, e: int, blocks: int) -> int:
     return int(lib().rsgpu_decode_workspace_bytes(k, e, blocks))
+
+
+def decode_general_workspace_bytes(k: int, m: int, nerrs: int, blocks: int) -> int:
+    return int(lib().rsgpu_decode_general_workspace_bytes(k, m, nerrs, blocks))
 
 
 def row_pitch(symbol_size: int) -> int:
@@ -374,8 +406,9 @@ class GpuDecoder:
     def __init__(self, symbols: int, symbol_size: int, encoded_symbols: int, blocks: int = 1,
                  seed: int = 1, ctx: Optional[Context] = None, device: int = 0,
                  block0: int = 0, pitch: Optional[int] = None,
-                 erasures: Optional[np.ndarray] = None):
+                 erasures: Optional[np.ndarray] = None, synchronous: bool = False):
         import torch
+        self.synchronous = synchronous
         if encoded_symbols > symbols:
             raise ValueError("erased symbols must be originals (<= symbols)")
         self.k, self.e, self.L, self.B = symbols, encoded_symbols, symbol_size, blocks
@@ -395,10 +428,16 @@ class GpuDecoder:
         self._decoded = False
 
     def decode_all(self, encoder: GpuEncoder) -> int:
+        """Enqueue the decode of every block.  Returns the processed payload
+        count; a synchronous decoder (the reference's shape) waits and returns
+        0 when any block's matrix was singular or its erasure list malformed,
+        as isa_decoder::decode_all does on "BAD MATRIX" (isa.cpp:185-190)."""
         assert encoder.payload_count() == self.e  # isa.cpp:171-172
         self.ctx.decode_blocks(self.k, self.e, self.L, self.pitch, self.B, encoder.src,
                                encoder.par, self.err, self.out, self.ws, self.status)
         self._decoded = True
+        if self.synchronous and not (self.block_status() == 0).all():
+            return 0
         return encoder.payload_count()
 
     def block_status(self) -> np.ndarray:
@@ -456,6 +495,9 @@ class ThroughputBenchmark:
     blocks: int = 1
     seed: int = 1
     ctx: Optional[Context] = None
+    # erasure lists [blocks][erased] replacing the drawn ones (a test hook:
+    # e.g. a malformed list, whose measurement must be rejected)
+    erasures: Optional[np.ndarray] = None
     results: List[Dict] = field(default_factory=list)
 
     def configurations(self) -> List[Config]:
@@ -475,7 +517,7 @@ class ThroughputBenchmark:
         enc = GpuEncoder(cfg.symbols, cfg.symbol_size, cfg.erased_symbols, self.blocks,
                          self.seed, ctx)
         dec = GpuDecoder(cfg.symbols, cfg.symbol_size, cfg.erased_symbols, self.blocks,
-                         self.seed, ctx)
+                         self.seed, ctx, erasures=self.erasures)
         encoded = recovered = processed = 0
         torch.cuda.synchronize()
         if cfg.type == "encoder":
@@ -491,6 +533,8 @@ class ThroughputBenchmark:
             processed += dec.decode_all(enc) * self.blocks
             torch.cuda.synchronize()
             t = time.perf_counter() - t0
+            # measurement() counts recovered bytes only for complete decodes
+            # (throughput_benchmark.hpp:185-196)
             if dec.is_complete():
                 recovered += cfg.erased_symbols * self.blocks
         else:

@@ -33,6 +33,19 @@ CASES = [
 ]
 BLOCKS = 2
 
+# general decode cases: (matrix, k, m, len, block, erased rows ascending)
+GENERAL = [
+    ("cauchy", 5, 9, 256, 7, [1, 3, 6, 8]),
+    ("rs", 10, 14, 4096, 1, [2, 4, 11, 13]),
+    ("cauchy", 12, 20, 2048, 2, [12, 13, 14, 15, 16, 17, 18, 19]),
+    ("rs", 64, 96, 4096, 3, [0, 5, 9, 17, 30, 31, 44, 63, 64, 70, 81, 95]),
+    ("rs", 100, 120, 2048, 4, [3, 50, 99, 100, 119]),
+    ("cauchy", 40, 72, 1024, 5, list(range(20, 52))),
+    ("rs", 144, 163, 1024, 6, [12, 16, 41, 49, 58, 68, 73, 75, 95, 97, 110, 113, 115, 145, 156]),
+    ("rs", 150, 177, 1024, 7, [1, 6, 34, 44, 46, 48, 51, 70, 83, 110, 111, 120, 130, 142, 157, 176]),
+    ("rs", 121, 137, 1024, 8, [2, 25, 26, 38, 42, 43, 44, 47, 48, 63, 84, 89, 90, 113, 117, 129]),
+]
+
 
 def sha(b: np.ndarray) -> str:
     return hashlib.sha256(np.ascontiguousarray(b).tobytes()).hexdigest()
@@ -81,6 +94,33 @@ def main() -> None:
     ref.encode_data(256, 5, 4, g, data, par)
     out["cauchy_9_5"] = {"matrix_hex": ca.tobytes().hex(), "blk": 7, "len": 256,
                          "parity_hex": [p.tobytes().hex() for p in par]}
+
+    # General decode (erasure_code_base_test.c:133-213 gf_gen_decode_matrix,
+    # the test's own static function compiled from the reference, and the
+    # recovery of :299-308): erasures among data AND parity rows, RS and
+    # Cauchy matrices; the two RS cases at k 144 / 150 take the singular-
+    # survivor retry, the k 121 case ends in "BAD MATRIX".
+    out["general_decode"] = []
+    for kind, k, m, L, blk, err in GENERAL:
+        enc = ref.gen_rs_matrix(m, k) if kind == "rs" else ref.gen_cauchy1_matrix(m, k)
+        data = [row for row in synth_block(SEED, blk, k, L)]
+        g = ref.init_tables(k, m - k, enc[k:])
+        par = [np.zeros(L, np.uint8) for _ in range(m - k)]
+        ref.encode_data(L, k, m - k, g, data, par)
+        rows = data + par
+        rc, dm, idx = ref.gen_decode_matrix(enc, err)
+        case = {"matrix": kind, "k": k, "m": m, "len": L, "blk": blk, "err": err, "rc": rc,
+                "parity_sha": [sha(p) for p in par]}
+        if rc == 0:
+            recov = [rows[i] for i in idx]
+            gd = ref.init_tables(k, len(err), dm)
+            rec = [np.zeros(L, np.uint8) for _ in err]
+            ref.encode_data(L, k, len(err), gd, recov, rec)
+            assert all((rec[i] == rows[err[i]]).all() for i in range(len(err)))
+            case["decode_index"] = idx.tolist()
+            case["decode_matrix_sha"] = sha(dm)
+            case["recovered_sha"] = [sha(r) for r in rec]
+        out["general_decode"].append(case)
 
     # KATs from erasure_code/gf_inverse_test.c:124-143, :172-179
     kat = {}

@@ -68,6 +68,10 @@ class Oracle:
         self._dec_block = L.fn("decode_block", C.c_int, C.c_int, C.c_int, C.c_int, u8p,
                                vpp, vpp, vpp)
         self._dec_matrix = L.fn("decode_matrix", C.c_int, C.c_int, C.c_int, u8p, u8p)
+        self._gen_dec = L.fn("gen_decode_matrix", C.c_int, u8p, C.c_int, C.c_int, u8p, C.c_int,
+                             u8p, u8p)
+        self._dec_general = L.fn("decode_general", C.c_int, u8p, C.c_int, C.c_int, C.c_int, u8p,
+                                 C.c_int, vpp, vpp)
         self.synth_word = L.fn("synth_word", C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64)
         self._synth_row = L.fn("synth_row", None, C.c_uint64, C.c_uint64, u8p, C.c_size_t)
         self._pattern = L.fn("erasure_pattern", None, C.c_uint64, C.c_uint64, C.c_int,
@@ -131,6 +135,30 @@ class Oracle:
         rc = self._dec_matrix(k, e, err.ctypes.data, c.ctypes.data)
         return rc, c[: k * e].reshape(e, k)
 
+    def gen_decode_matrix(self, encode_matrix: np.ndarray, err_list):
+        """erasure_code_base_test.c:133-213 -> (rc, decode_matrix [nerrs][k],
+        decode_index [k]); rc -2 = NO_INVERT_MATRIX."""
+        m, k = encode_matrix.shape
+        enc = np.ascontiguousarray(encode_matrix, np.uint8)
+        err = np.ascontiguousarray(err_list, np.uint8)
+        dm = np.zeros(max(1, len(err)) * k, np.uint8)
+        idx = np.zeros(k, np.int32)
+        rc = self._gen_dec(enc.ctypes.data, k, m, err.ctypes.data, len(err), dm.ctypes.data,
+                           idx.ctypes.data)
+        return rc, dm[: len(err) * k].reshape(len(err), k), idx
+
+    def decode_general(self, encode_matrix: np.ndarray, rows, err_list):
+        """Recover rows err_list (data and parity) from the m rows `rows` (the
+        erased ones are not read) -> (rc, [nerrs rows])."""
+        m, k = encode_matrix.shape
+        enc = np.ascontiguousarray(encode_matrix, np.uint8)
+        err = np.ascontiguousarray(err_list, np.uint8)
+        L = rows[0].shape[0]
+        out = [np.zeros(L, np.uint8) for _ in range(len(err))]
+        rc = self._dec_general(enc.ctypes.data, k, m, L, err.ctypes.data, len(err), _ptrs(rows),
+                               _ptrs(out))
+        return rc, out
+
     def synth_row(self, seed: int, row: int, length: int) -> np.ndarray:
         d = np.zeros(length, np.uint8)
         self._synth_row(seed, row, d.ctypes.data, length)
@@ -171,6 +199,20 @@ class Reference:
         self._dec_avx2 = L.fn("decode_block_avx2", C.c_int, C.c_int, C.c_int, C.c_int, u8p,
                               vpp, vpp, vpp)
         self.have_avx2 = bool(L.fn("have_avx2", C.c_int)())
+        # erasure_code_base_test.c's own static gf_gen_decode_matrix
+        # (ref_decode_matrix.c)
+        self._gen_dec = L.fn("gf_gen_decode_matrix", C.c_int, u8p, u8p, u8p, u8p, C.c_int,
+                             C.c_int, C.c_int)
+
+    def gen_decode_matrix(self, encode_matrix: np.ndarray, err_list):
+        m, k = encode_matrix.shape
+        enc = np.ascontiguousarray(encode_matrix, np.uint8).copy()
+        err = np.ascontiguousarray(err_list, np.uint8).copy()
+        dm = np.zeros(max(1, len(err)) * k, np.uint8)
+        idx = np.zeros(k, np.uint32)
+        rc = self._gen_dec(enc.ctypes.data, dm.ctypes.data, idx.ctypes.data, err.ctypes.data,
+                           len(err), k, m)
+        return rc, dm[: len(err) * k].reshape(len(err), k), idx.astype(np.int32)
 
     gen_rs_matrix = Oracle.gen_rs_matrix
     gen_cauchy1_matrix = Oracle.gen_cauchy1_matrix

@@ -1,8 +1,8 @@
 """The generated GF(2^8) asm (storage-benchmarks_amd/csrc/gen_tc_handlers.py)
 checked on the CPU by interpreting its VALU instructions over bit-sliced
-planes: the 256 threaded-code handlers, the compile-time syndrome MAC blocks,
-the Horner twiddles and the parity pre-scales must multiply exactly as
-gf_mul (isa/ec_base.c:36-48) does.  No GPU needed: a wrong register or plane
+planes: the 256 threaded-code handlers, the chunk dispatch, and the encode's
+per-source XOR programs and Horner twiddles (gen_enc_progs.py) must multiply
+exactly as gf_mul (isa/ec_base.c:36-48) does.  No GPU needed: a wrong register or plane
 in the generator shows up here before it can corrupt a decode."""
 import os
 import random
@@ -78,60 +78,6 @@ def test_handler_multiplies(c):
 def test_handler_table_layout():
     tbl = g.handler_table()
     assert sum(4 if i.startswith("s_") else 8 for i in tbl) == g.NHANDLERS * g.STRIDE
-
-
-def test_lin_inplace_all_constants():
-    rng = random.Random(7)
-    for c in range(1, 256):
-        for slot in (0, 5):
-            regs = {i: 0 for i in range(256)}
-            by = [rng.randrange(256) for _ in range(32)]
-            base = g.ACC + 8 * slot
-            for a, v in enumerate(planes(by)):
-                regs[base + a] = v
-            run(g.lin_inplace(c, slot), regs)
-            assert unplanes([regs[base + a] for a in range(8)]) == [g.gf_mul(c, x) for x in by]
-
-
-@pytest.mark.parametrize("plan", g.SYN_PLANS, ids=lambda p: "K%dE%dC%d" % p)
-def test_syndrome_blocks_horner(plan):
-    """The fused decode's phase 1 (rs_decode_fused.hip) as the kernel runs
-    it: parity rows pre-scaled in the accumulators, then the live sources in
-    Horner order (chunks NCH-1 .. 0) through the SynBlock MACs with one
-    twiddle per chunk boundary -- equals P_r ^ sum_{j live} 2^(r j) d_j."""
-    K, E, C = plan
-    rng = random.Random(K * 1000 + E * 10 + C)
-    data = [[rng.randrange(256) for _ in range(32)] for _ in range(K)]
-    par = [[rng.randrange(256) for _ in range(32)] for _ in range(E)]
-    nch = (K + C - 1) // C
-    erased = set(rng.sample(range(K), E))
-    live = [j for j in range(K) if j not in erased]
-    for grp in range((E + 7) // 8):
-        regs = {i: 0 for i in range(256)}
-        for s in range(8):
-            r = 8 * grp + s
-            if r < E:
-                for a, v in enumerate(planes(par[r])):
-                    regs[g.ACC + 8 * s + a] = v
-        run(g.syn_prescale(K, E, C, grp), regs)
-        for ch in reversed(range(nch)):
-            if ch != nch - 1:
-                run(g.syn_twiddle(E, C, grp), regs)
-            for t in range(C):
-                j = ch * C + t
-                if j < K and j not in erased:
-                    load_tables(regs, data[j])
-                    run(g.syn_block(K, E, grp, t), regs)
-        for s in range(8):
-            r = 8 * grp + s
-            if r >= E:
-                continue
-            exp = list(par[r])
-            for j in live:
-                cj = g.gf_pow2(r * j)
-                exp = [x ^ g.gf_mul(cj, y) for x, y in zip(exp, data[j])]
-            got = unplanes([regs[g.ACC + 8 * s + a] for a in range(8)])
-            assert got == exp, (plan, r)
 
 
 DS = re.compile(r"ds_read_b128 v\[(\d+):(\d+)\], %\[la\] offset:(\d+)")

@@ -315,18 +315,16 @@ def test_plugin_dropin_reference_shape():
     assert r.stdout.count("complete=1 verified=1") == 6, r.stdout
 
 
-@pytest.mark.parametrize("mode", ["fused", "split", "direct"])
+@pytest.mark.parametrize("mode", ["fused", "one_matrix", "general"])
 def test_decode_modes_end_to_end(mode):
-    """Every decode kernel choice of the syndrome path (RSGPU_DECODE, read
-    once per process -- hence a child process per mode): the one-matrix
-    k_rs_tc decode (default), the fused syndrome + solve kernel, and the
-    split syndrome kernel + in-place solve, through the reference-shaped
-    plugin with device verification of every recovered byte."""
+    """Every decode kernel choice (rsgpu_set_decode_kernel): the one-matrix
+    k_rs_tc decode (default), the fused syndrome + solve kernel and the
+    general k x k inversion, through the reference-shaped plugin with device
+    verification of every recovered byte."""
     import subprocess
     exe = os.path.join(os.path.dirname(HERE), "storage-benchmarks_amd", "bin", "plugin_dropin_test")
-    env = dict(os.environ, RSGPU_DECODE=mode)
-    r = subprocess.run([exe, "16:64000:8", "64:1000000:32", "100:64000:20", "64:32000:32", "20:4096:7"],
-                       capture_output=True, text=True, timeout=300, env=env)
+    r = subprocess.run([exe, "--decode-kernel", mode, "16:64000:8", "64:1000000:32", "100:64000:20",
+                        "64:32000:32", "20:4096:7"], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert r.stdout.count("complete=1 verified=1") == 5, r.stdout
 
@@ -438,12 +436,14 @@ def test_ec_encode_data_row_passes(ctx, orc, length, per):
     assert not bad, f"rows {bad} differ"
 
 
-def test_host_io_pipelined_ragged_chunks(ctx):
+def test_host_io_ragged_chunks(ctx):
     """bench.host_io_pipelined (the overlapped PCIe-inclusive path): 6 blocks
     in chunks of 4 (a ragged last chunk), survivors shipped as row runs; the
     recovered rows on the device equal the originals and the host copies
-    equal the device rows."""
+    equal the device rows.  The serial host_io_rate ships the same bytes."""
     sys.path.insert(0, os.path.dirname(HERE))
     import bench
     r = bench.host_io_pipelined(rsgpu, ctx, 16, 8, 64000, 6, seed=3, chunk=4, reps=1)
     assert r["verified"] and r["blocks"] == 6
+    s = bench.host_io_rate(rsgpu, ctx, 16, 8, 64000, 6, seed=3, reps=1)
+    assert s["verified"] and s["poisoned"]

@@ -170,3 +170,56 @@ def test_avx2_port_equals_reference_base():
         assert rc1 == rc2 == 0
         assert all((x == y).all() for x, y in zip(r1, r2))
         assert all((r2[i] == data[s]).all() for i, s in enumerate(err))
+
+
+def _general_rows(orc, case):
+    k, m, L = case["k"], case["m"], case["len"]
+    enc = orc.gen_rs_matrix(m, k) if case["matrix"] == "rs" else orc.gen_cauchy1_matrix(m, k)
+    data = list(synth_block(GOLD["seed"], case["blk"], k, L))
+    g = orc.init_tables(k, m - k, enc[k:])
+    par = [np.zeros(L, np.uint8) for _ in range(m - k)]
+    orc.encode_data(L, k, m - k, g, data, par)
+    return enc, data + par
+
+
+@pytest.mark.parametrize("case", GOLD["general_decode"],
+                         ids=lambda c: f"{c['matrix']}k{c['k']}m{c['m']}n{len(c['err'])}")
+def test_golden_general_decode(orc, case):
+    """gf_gen_decode_matrix restated (erasure_code_base_test.c:133-213) ==
+    the reference's own function on the golden cases: status, survivor
+    choice (including the singular-survivor retry and "BAD MATRIX"), decode
+    matrix and recovered rows (data and parity erasures)."""
+    enc, rows = _general_rows(orc, case)
+    k = case["k"]
+    assert [sha(p) for p in rows[k:]] == case["parity_sha"]
+    rc, dm, idx = orc.gen_decode_matrix(enc, case["err"])
+    assert rc == case["rc"]
+    if rc != 0:
+        return
+    assert idx.tolist() == case["decode_index"]
+    assert sha(dm) == case["decode_matrix_sha"]
+    rc2, rec = orc.decode_general(enc, rows, case["err"])
+    assert rc2 == 0
+    assert [sha(r) for r in rec] == case["recovered_sha"]
+    assert all((rec[i] == rows[j]).all() for i, j in enumerate(case["err"]))
+
+
+@needs_ref
+def test_general_decode_matrix_vs_reference_random():
+    """Random RS / Cauchy codes and erasure lists over data and parity rows:
+    the restatement equals the reference's gf_gen_decode_matrix (compiled
+    from erasure_code_base_test.c by oracle/Makefile) in status, survivors
+    and matrix."""
+    orc, ref = Oracle(), Reference()
+    rng = np.random.default_rng(13)
+    for trial in range(400):
+        k = int(rng.integers(1, 60))
+        p = int(rng.integers(1, 24))
+        m = k + p
+        enc = orc.gen_rs_matrix(m, k) if trial % 2 else orc.gen_cauchy1_matrix(m, k)
+        n = int(rng.integers(1, p + 1))
+        err = np.sort(rng.choice(m, n, replace=False)).astype(np.uint8)
+        a, b = orc.gen_decode_matrix(enc, err), ref.gen_decode_matrix(enc, err)
+        assert a[0] == b[0]
+        if a[0] == 0:
+            assert (a[1] == b[1]).all() and (a[2] == b[2]).all()
