@@ -65,7 +65,7 @@ def parse(argv=None):
     p.add_argument("--batch", type=int, default=C4_BATCH, help="c4: resident blocks per batch")
     p.add_argument("--seed", type=int, default=1)
     p.add_argument("--decode-kernel", default="auto",
-                   choices=["auto", "one_matrix", "fused", "general"])
+                   choices=["auto", "generated", "one_matrix", "fused", "general"])
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-threads", type=int, default=None)
     p.add_argument("--no-ref-base", action="store_true",
@@ -407,7 +407,7 @@ def alg_bytes(k, e, L):
     blk_op = float((k + e) * L)
     return {"k_rs_bs(encode)": blk_op, "k_rs_encode_lh": blk_op, "k_dot_generic": blk_op,
             "k_dot_generic(decode)": blk_op, "k_rs_decode_fused": blk_op,
-            "k_rs_tc(encode)": blk_op, "k_rs_tc(decode)": blk_op,
+            "k_rs_tc(encode)": blk_op, "k_rs_tc(decode)": blk_op, "k_rs_jit(decode)": blk_op,
             "k_decode_prepare": 0.0, "k_decode_prepare_syn": 0.0}
 
 

@@ -140,6 +140,7 @@ size_t rsgpu_decode_workspace_bytes(int k, int e, size_t blocks);
 #define RSGPU_DECODE_ONE_MATRIX 1
 #define RSGPU_DECODE_FUSED 2
 #define RSGPU_DECODE_GENERAL 3
+#define RSGPU_DECODE_GENERATED 4
 int rsgpu_set_decode_kernel(rsgpu_ctx *ctx, int kernel);
 
 /* isa_decoder::decode_all over `blocks` blocks (isa.cpp:169-213): for block

@@ -1,0 +1,177 @@
+// rs_jit.h -- per-block generated decode code (k_rs_jit, rs_jit.hip).
+//
+// The one-matrix decode applies an e x k coefficient matrix that differs per
+// block (random erasures).  k_rs_tc dispatches each coefficient through a
+// handler (a jump, SALU work and GPR-index mode per coefficient); here the
+// prepare kernel instead WRITES the straight-line code of every (block,
+// wave, chunk of 8 sources) into executable device memory, with the
+// coefficients baked into the register operands, and the decode kernel
+// makes one call per chunk.  Only vector-ALU, LDS-read, s_waitcnt, s_nop
+// and s_setpc instructions are ever generated.
+//
+// Register contract (the decode kernel's asm statement clobbers all of it):
+//   v20            LDS byte address of the chunk's first source + 16 lane
+//   v24..v31       planes of the current source, bank A: L1 L2 L4 L8 H1 H2
+//                  H4 H8 (plane a of the 32 bytes of a lane, bit-sliced as in
+//                  rs_bitsliced.hip / bitslice.h tr8)
+//   v54..v61       the same, bank B (odd sources: the next source's planes
+//                  land in the other bank while this one is consumed)
+//   v32..v42       composite four-Russians entries L[n], n = 3 5 6 7 9 ... 15
+//   v43..v53       composite entries H[n]
+//   v64..v127      accumulators: slot s (output row 8 w + s) planes v[64+8s ..]
+//   s[82:83]       return address (s_swappc_b64 s[82:83], code)
+//
+// Code of one chunk (nt <= 8 sources, nslot <= 8 output rows of the wave):
+//   prologue   ds_read_b128 x2: source 0's planes into bank A      16 B
+//   source t   [ds_read_b128 x2 of source t+1 into bank (t+1)&1, or 2 x
+//              (s_nop; s_nop)], s_waitcnt lgkmcnt(2 or 0), 22 v_xor_b32
+//              composites from bank t&1, s_nop, then per slot 8
+//              multiply-accumulates of 8 bytes each (v_bitop3_b32 0x96 /
+//              v_xor_b32_e64 / s_nop pair for a zero row)       112 + 64 nslot B
+//   epilogue   s_setpc_b64 s[82:83]; s_nop                           8 B
+// The layout depends on (nt, nslot) only, never on the coefficients.
+#pragma once
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#define RJ_HD __host__ __device__
+#else
+#define RJ_HD
+#endif
+
+namespace rsgpu {
+namespace jit {
+
+constexpr int ACC = 64;          // accumulator base register
+constexpr int LDS_SRC = 2048;    // LDS bytes per source: [2 halves][64 lanes] x 16 B
+constexpr int LDS_HALF = 1024;
+constexpr int PRO_BYTES = 16;
+constexpr int PRE_BYTES = 112;   // per source before the multiply-accumulates
+constexpr int EPI_BYTES = 8;
+
+RJ_HD constexpr int src_bytes(int nslot) { return PRE_BYTES + 64 * nslot; }
+RJ_HD constexpr int chunk_bytes(int nt, int nslot) { return PRO_BYTES + nt * src_bytes(nslot) + EPI_BYTES; }
+// stride between chunks: the largest chunk, rounded to 64-byte lines
+RJ_HD constexpr int chunk_stride(int nslot) { return (chunk_bytes(8, nslot) + 63) / 64 * 64; }
+
+// plane registers of bank `bank`: entry 0..3 = L1 L2 L4 L8, 4..7 = H1 H2 H4 H8
+RJ_HD constexpr int plane_reg(int bank, int a) { return (bank ? 54 : 24) + a; }
+
+// four-Russians table register of L[n] (hi = 0) or H[n] (hi = 1), n = 1..15
+RJ_HD constexpr int table_reg(int bank, int hi, int n)
+{
+    if ((n & (n - 1)) == 0) {  // single plane
+        const int a = n == 1 ? 0 : n == 2 ? 1 : n == 4 ? 2 : 3;
+        return plane_reg(bank, 4 * hi + a);
+    }
+    // composites n = 3 5 6 7 9 10 11 12 13 14 15 -> 0..10
+    int idx = 0;
+    for (int m = 3; m < n; ++m)
+        idx += (m & (m - 1)) != 0;
+    return 32 + 11 * hi + idx;
+}
+
+// ---- gfx950 encodings (llvm-mc -mcpu=gfx950 -show-encoding) -------------
+
+RJ_HD inline uint64_t enc_bitop3_96(int d, int a, int b, int c)  // d = a ^ b ^ c
+{
+    const uint32_t w0 = 0xd2340200u | (uint32_t)d;
+    const uint32_t w1 = 0xd0000000u | ((uint32_t)(256 + c) << 18) | ((uint32_t)(256 + b) << 9) |
+                        (uint32_t)(256 + a);
+    return (uint64_t)w1 << 32 | w0;
+}
+RJ_HD inline uint64_t enc_xor_e64(int d, int a, int b)  // VOP3 form, 8 bytes
+{
+    const uint32_t w0 = 0xd1150000u | (uint32_t)d;
+    const uint32_t w1 = ((uint32_t)(256 + b) << 9) | (uint32_t)(256 + a);
+    return (uint64_t)w1 << 32 | w0;
+}
+RJ_HD inline uint32_t enc_xor_e32(int d, int a, int b)  // VOP2, 4 bytes
+{
+    return 0x2a000000u | ((uint32_t)d << 17) | ((uint32_t)b << 9) | (uint32_t)(256 + a);
+}
+RJ_HD inline uint64_t enc_ds_read_b128(int vd, int vaddr, int offset)
+{
+    return (uint64_t)(((uint32_t)vd << 24) | (uint32_t)vaddr) << 32 | (0xd9fe0000u | (uint32_t)offset);
+}
+constexpr uint32_t S_NOP0 = 0xbf800000u;
+constexpr uint32_t S_SETPC_82 = 0xbe801d52u;  // s_setpc_b64 s[82:83]
+RJ_HD inline uint32_t enc_waitcnt_lgkm(int n) { return 0xbf8cc07fu | ((uint32_t)n << 8); }
+
+// row b of the 8 x 8 GF(2) matrix of x -> c x: bit a set iff bit b of c 2^a
+RJ_HD inline void mat_rows(uint8_t c, uint8_t (&row)[8])
+{
+    uint8_t p[8];
+    uint8_t x = c;
+    for (int a = 0; a < 8; ++a) {
+        p[a] = x;
+        x = (uint8_t)((x << 1) ^ ((x & 0x80) ? 0x1D : 0));
+    }
+    for (int b = 0; b < 8; ++b) {
+        uint8_t r = 0;
+        for (int a = 0; a < 8; ++a)
+            r |= (uint8_t)(((p[a] >> b) & 1) << a);
+        row[b] = r;
+    }
+}
+
+// Writes the 64 multiply-accumulate bytes of coefficient c on slot s, bank
+// `bank`, at dst (8-byte aligned): acc_b ^= L[m_b & 15] ^ H[m_b >> 4].
+RJ_HD inline void emit_mac(uint64_t* dst, uint8_t c, int s, int bank)
+{
+    uint8_t row[8];
+    mat_rows(c, row);
+    for (int b = 0; b < 8; ++b) {
+        const int acc = ACC + 8 * s + b, lo = row[b] & 15, hi = row[b] >> 4;
+        if (lo && hi)
+            dst[b] = enc_bitop3_96(acc, acc, table_reg(bank, 0, lo), table_reg(bank, 1, hi));
+        else if (lo)
+            dst[b] = enc_xor_e64(acc, acc, table_reg(bank, 0, lo));
+        else if (hi)
+            dst[b] = enc_xor_e64(acc, acc, table_reg(bank, 1, hi));
+        else  // c == 0
+            dst[b] = (uint64_t)S_NOP0 << 32 | S_NOP0;
+    }
+}
+
+// Writes the 112-byte preamble of source t (of nt) at dst (8-byte aligned):
+// the next source's plane loads (or no-ops), the wait for this source's
+// planes, the 22 composites, one s_nop.
+RJ_HD inline void emit_pre(uint64_t* dst, int t, int nt)
+{
+    uint32_t* w = reinterpret_cast<uint32_t*>(dst);
+    const int bank = t & 1, nb = (t + 1) & 1;
+    if (t + 1 < nt) {
+        const uint64_t a = enc_ds_read_b128(plane_reg(nb, 0), 20, (t + 1) * LDS_SRC);
+        const uint64_t b = enc_ds_read_b128(plane_reg(nb, 4), 20, (t + 1) * LDS_SRC + LDS_HALF);
+        w[0] = (uint32_t)a;
+        w[1] = (uint32_t)(a >> 32);
+        w[2] = (uint32_t)b;
+        w[3] = (uint32_t)(b >> 32);
+        w[4] = enc_waitcnt_lgkm(2);  // this source's two loads done, the next two in flight
+    } else {
+        w[0] = w[1] = w[2] = w[3] = S_NOP0;
+        w[4] = enc_waitcnt_lgkm(0);
+    }
+    int i = 5;
+    for (int hi = 0; hi < 2; ++hi)
+        for (int n = 1; n < 16; ++n) {
+            const int low = n & -n;
+            if (n != low)
+                w[i++] = enc_xor_e32(table_reg(bank, hi, n), table_reg(bank, hi, n ^ low),
+                                     table_reg(bank, hi, low));
+        }
+    w[i++] = S_NOP0;  // i == 28: 112 bytes
+}
+
+// prologue (source 0's planes into bank A) at the chunk start
+RJ_HD inline void emit_prologue(uint64_t* dst)
+{
+    dst[0] = enc_ds_read_b128(plane_reg(0, 0), 20, 0);
+    dst[1] = enc_ds_read_b128(plane_reg(0, 4), 20, LDS_HALF);
+}
+
+RJ_HD inline void emit_epilogue(uint64_t* dst) { dst[0] = (uint64_t)S_NOP0 << 32 | S_SETPC_82; }
+
+}  // namespace jit
+}  // namespace rsgpu

@@ -1,0 +1,196 @@
+// rs_jit.hip -- the one-matrix decode through per-block generated code
+// (rs_jit.h): dsts[b][i] = sum_p c_b[i][p] * srcs[b][p] with the e x k matrix
+// of block b baked into code that k_decode_prepare_syn wrote into executable
+// device memory (rsgpu_capi.cpp allocates it from the GPU's coarse-grained
+// pool with HSA_AMD_MEMORY_POOL_EXECUTABLE_FLAG).
+//
+// Work split as k_rs_tc (rs_tc.hip): a workgroup of NW waves covers one 2 KB
+// column tile (64 lanes x 32 bytes) of every row of one block; wave w owns
+// output rows [8w, 8w+8); the waves share the loading (LDS-DMA) and bit
+// transposing of each chunk of 8 sources through LDS.  Per chunk a wave makes
+// ONE call into its generated code, which reads the planes from LDS, builds
+// the four-Russians tables and applies its 8 x 8 coefficients: no
+// per-coefficient jumps, no scalar loads of handler addresses, no GPR index
+// mode.
+//
+// The instruction cache is not invalidated between kernel launches, and the
+// code of a block is rewritten by every prepare, so each wave executes
+// s_icache_inv before its first call (measured free: tools/ubench_jit.hip).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <utility>
+
+#include "bitslice.h"
+#include "rs_jit.h"
+#include "rs_kernels.h"
+#include "tc_handlers.inc"
+
+namespace rsgpu {
+namespace jitk {
+
+using bs::barrier_lds;
+using bs::glds32;
+using bs::sload_ptr;
+using bs::store32;
+using bs::tr8;
+using bs::vconst;
+using bs::wait_vm;
+
+constexpr int C = 8;  // sources per LDS chunk (double-buffered)
+
+template <int S>
+__device__ __forceinline__ void read_slot(uint32_t (&W)[8])
+{
+    uint64_t P[4];
+#define RSGPU_JIT_RD(TEXT) asm volatile(TEXT : "=v"(P[0]), "=v"(P[1]), "=v"(P[2]), "=v"(P[3]))
+    if constexpr (S == 0) RSGPU_JIT_RD(RSGPU_TC_READ_SLOT64_0);
+    if constexpr (S == 1) RSGPU_JIT_RD(RSGPU_TC_READ_SLOT64_1);
+    if constexpr (S == 2) RSGPU_JIT_RD(RSGPU_TC_READ_SLOT64_2);
+    if constexpr (S == 3) RSGPU_JIT_RD(RSGPU_TC_READ_SLOT64_3);
+    if constexpr (S == 4) RSGPU_JIT_RD(RSGPU_TC_READ_SLOT64_4);
+    if constexpr (S == 5) RSGPU_JIT_RD(RSGPU_TC_READ_SLOT64_5);
+    if constexpr (S == 6) RSGPU_JIT_RD(RSGPU_TC_READ_SLOT64_6);
+    if constexpr (S == 7) RSGPU_JIT_RD(RSGPU_TC_READ_SLOT64_7);
+#undef RSGPU_JIT_RD
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        W[2 * q] = (uint32_t)P[q];
+        W[2 * q + 1] = (uint32_t)(P[q] >> 32);
+    }
+}
+
+// amdgpu_num_vgpr(64): the compiler allocates v0..v63 only (minus the
+// registers the call clobbers); the accumulators v64..v127 are touched by asm
+// and generated code alone.
+template <int NW>
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_num_vgpr(64))) void k_rs_jit(JitArgs a)
+{
+    __shared__ uint4 lds[2][C * 2 * 64];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int b = blockIdx.y;
+    if (a.status[b] != 0)
+        return;  // uniform per workgroup: the whole block is skipped
+    const int k = a.k;
+    const int nch = (k + C - 1) / C;
+    const long long tile = blockIdx.x;
+    const uint8_t* const* srcs = a.srcs + (size_t)b * k;
+    uint8_t* const* dsts = a.dsts + (size_t)b * a.rows;
+    // this wave's generated code: chunk ch at code + ch * stride
+    const uint8_t* code = a.code + ((size_t)b * NW + wave) * (size_t)nch * a.chunk_stride;
+    const uint32_t m4 = vconst(0x0F0F0F0Fu), m2 = vconst(0x33333333u), m1 = vconst(0x55555555u);
+    const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint4*)&lds[0][0];
+    const long long off = tile * 2048 + lane * 32;
+    const long long loff = off + 32 <= a.len ? off : 0;  // out-of-range lanes re-read the row head
+
+    asm volatile("s_icache_inv\n s_nop 15\n s_nop 15" ::: "memory");
+
+    auto issue = [&](int ch) {
+        const int c0 = ch * C, nt = min(C, k - c0);
+        const uint32_t base = lds0 + (uint32_t)((ch & 1) * C * 2 * 64 * 16);
+        int t = wave;
+        for (; t + NW < nt; t += 2 * NW) {
+            const uint8_t *r0, *r1;
+            asm volatile("s_load_dwordx2 %0, %2, 0\n s_load_dwordx2 %1, %3, 0\n s_waitcnt lgkmcnt(0)"
+                         : "=&s"(r0), "=&s"(r1)
+                         : "s"(srcs + c0 + t), "s"(srcs + c0 + t + NW)
+                         : "memory");
+            glds32(r0, (uint32_t)loff, base + (uint32_t)(t * 2 * 64 * 16));
+            glds32(r1, (uint32_t)loff, base + (uint32_t)((t + NW) * 2 * 64 * 16));
+        }
+        if (t < nt)
+            glds32(sload_ptr(srcs + c0 + t), (uint32_t)loff, base + (uint32_t)(t * 2 * 64 * 16));
+    };
+
+    asm volatile(RSGPU_TC_ZERO ::: RSGPU_TC_ACC_CLOBBERS);
+    issue(0);
+    for (int ch = 0; ch < nch; ++ch) {
+        const int nt = min(C, k - ch * C);
+        uint4* buf = lds[ch & 1];
+        wait_vm(0);  // this chunk's own sources, issued behind the previous barrier
+        // own share of this chunk: bytes -> bit-planes, in place
+        for (int t = wave; t < nt; t += NW) {
+            uint4 u = buf[(t * 2 + 0) * 64 + lane];
+            uint4 v = buf[(t * 2 + 1) * 64 + lane];
+            uint32_t W[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
+            tr8(W, m4, m2, m1);
+            buf[(t * 2 + 0) * 64 + lane] = make_uint4(W[0], W[1], W[2], W[3]);
+            buf[(t * 2 + 1) * 64 + lane] = make_uint4(W[4], W[5], W[6], W[7]);
+        }
+        barrier_lds();
+        // one barrier per chunk: every wave is past its call of chunk ch - 1,
+        // which read buffer (ch + 1) & 1, so chunk ch + 1 may land there now
+        if (ch + 1 < nch)
+            issue(ch + 1);
+        const uint32_t la = lds0 + (uint32_t)((ch & 1) * C * 2 * 64 * 16) + lane * 16;
+        const uint8_t* fn = code + (size_t)ch * a.chunk_stride;
+        asm volatile("s_swappc_b64 s[82:83], %[fn]"
+                     :
+                     : [fn] "s"(fn), "{v20}"(la)
+                     : "v24", "v25", "v26", "v27", "v28", "v29", "v30", "v31", "v32", "v33", "v34",
+                       "v35", "v36", "v37", "v38", "v39", "v40", "v41", "v42", "v43", "v44", "v45",
+                       "v46", "v47", "v48", "v49", "v50", "v51", "v52", "v53", "v54", "v55", "v56",
+                       "v57", "v58", "v59", "v60", "v61", "s82", "s83", "scc", "memory",
+                       RSGPU_TC_ACC_CLOBBERS);
+    }
+    // outputs back to bytes and out (every source of this tile was read
+    // before the last barrier)
+    if (off + 32 <= a.len) {
+        [&]<int... Ss>(std::integer_sequence<int, Ss...>) {
+            (
+                [&] {
+                    const int r = wave * 8 + Ss;
+                    if (r < a.rows) {
+                        uint32_t W[8];
+                        read_slot<Ss>(W);
+                        tr8(W, m4, m2, m1);
+                        store32((uint8_t*)sload_ptr((const uint8_t* const*)(dsts + r)), off, W);
+                    }
+                }(),
+                ...);
+        }(std::make_integer_sequence<int, 8>{});
+    }
+}
+
+// every 8-byte slot a return: a call that lands in code never written
+// comes straight back
+__global__ void k_jit_fill(uint64_t* code, long long n)
+{
+    const uint64_t ret = (uint64_t)jit::S_NOP0 << 32 | jit::S_SETPC_82;
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (long long)gridDim.x * blockDim.x)
+        code[i] = ret;
+}
+
+}  // namespace jitk
+
+size_t jit_code_bytes(int k, int e, long long blocks)
+{
+    const int nw = (e + 7) / 8, nch = (k + 7) / 8;
+    return (size_t)blocks * nw * nch * jit::chunk_stride(8);
+}
+
+hipError_t launch_jit_fill(void* code, size_t bytes, hipStream_t st)
+{
+    hipLaunchKernelGGL(jitk::k_jit_fill, dim3(4096), dim3(256), 0, st, (uint64_t*)code,
+                       (long long)(bytes / 8));
+    return hipGetLastError();
+}
+
+hipError_t launch_rs_jit(const JitArgs& a, long long blocks, hipStream_t st)
+{
+    if (a.rows <= 0 || a.rows > 32 || a.k <= 0 || !a.code || !a.status)
+        return hipErrorInvalidValue;
+    const int nw = (a.rows + 7) / 8;
+    dim3 grid((unsigned)((a.len + 2047) / 2048), (unsigned)blocks);
+    switch (nw) {
+    case 1: hipLaunchKernelGGL(jitk::k_rs_jit<1>, grid, dim3(64), 0, st, a); break;
+    case 2: hipLaunchKernelGGL(jitk::k_rs_jit<2>, grid, dim3(128), 0, st, a); break;
+    case 3: hipLaunchKernelGGL(jitk::k_rs_jit<3>, grid, dim3(192), 0, st, a); break;
+    default: hipLaunchKernelGGL(jitk::k_rs_jit<4>, grid, dim3(256), 0, st, a); break;
+    }
+    return hipGetLastError();
+}
+
+}  // namespace rsgpu

@@ -79,13 +79,31 @@ hipError_t launch_rs_bitsliced(int k, int e, const uint8_t* src, uint8_t* out, l
 //                        syn_addr [B][k-e][slots] of the syndrome rows
 //                        2^(r j) per surviving original j (ascending)
 // slots = tc_rows_per_pass(e); tc_table = the context's handler addresses.
+// jit_code != nullptr (with dir_addr == nullptr, one-matrix form): instead of
+// handler addresses, the straight-line code of k_rs_jit (rs_jit.h) for every
+// (block, wave, chunk) at jit_code + ((b NW + w) nch + ch) jit::chunk_stride(8).
 hipError_t launch_decode_prepare_syn(int k, int e, long long blocks, const uint8_t* err,
                                      uint8_t* out, long long out_pitch, const uint8_t** srcs,
                                      uint8_t** dsts, const unsigned long long* tc_table,
                                      unsigned long long* tc_addr, unsigned long long* emask,
                                      int* status, unsigned long long* syn_addr,
                                      const uint8_t* src, const uint8_t* par,
-                                     unsigned long long* dir_addr, hipStream_t st);
+                                     unsigned long long* dir_addr, uint8_t* jit_code,
+                                     hipStream_t st);
+
+// The one-matrix decode through generated code (rs_jit.hip).
+struct JitArgs {
+    const uint8_t* const* srcs;      // [B][k]
+    uint8_t* const* dsts;            // [B][rows]
+    const uint8_t* code;             // executable, written by k_decode_prepare_syn
+    long long chunk_stride;          // jit::chunk_stride(8)
+    int k, rows;                     // rows <= 32
+    long long len;                   // % 32 == 0
+    const int* status;               // [B]
+};
+size_t jit_code_bytes(int k, int e, long long blocks);
+hipError_t launch_jit_fill(void* code, size_t bytes, hipStream_t st);
+hipError_t launch_rs_jit(const JitArgs& a, long long blocks, hipStream_t st);
 
 // Threaded-code bit-sliced dot product with runtime coefficients (rs_tc.hip):
 // dsts[b][i] = sum_p c_b[i][p] * srcs[b][p] for rows <= 32 per launch, where

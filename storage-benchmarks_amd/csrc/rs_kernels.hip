@@ -34,6 +34,7 @@
 #include <utility>
 
 #include "gf256.h"
+#include "rs_jit.h"
 #include "rs_kernels.h"
 #include "rs_synth.h"
 
@@ -873,7 +874,8 @@ __global__ __launch_bounds__(256) void k_decode_prepare_syn(int k, int e,
                                                             unsigned long long* emask, int* status,
                                                             unsigned long long* syn_addr,
                                                             const uint8_t* src, const uint8_t* par,
-                                                            unsigned long long* dir_addr)
+                                                            unsigned long long* dir_addr,
+                                                            uint8_t* jit_code)
 {
     extern __shared__ __align__(16) uint8_t lds[];
     uint8_t* gexp = lds;          // 512
@@ -916,7 +918,7 @@ __global__ __launch_bounds__(256) void k_decode_prepare_syn(int k, int e,
         return (x && y) ? gexp[glog[x] + glog[y]] : (uint8_t)0;
     };
     const int tc_rows = tc_rows_per_pass(e);
-    if (dir_addr) {
+    if (dir_addr || jit_code) {
         // One-matrix decode through k_rs_tc: sources = the k - e surviving
         // originals (ascending) then the e parity rows, outputs = the erased
         // originals.  d_E = V_E^-1 (P ^ V_kept d_kept), V_E[p][i] = a_i^p with
@@ -993,19 +995,47 @@ __global__ __launch_bounds__(256) void k_decode_prepare_syn(int k, int e,
                                              : par + ((size_t)b * e + (q - nl)) * out_pitch;
         for (int i = tid; i < e; i += nt)
             dsts[(size_t)b * e + i] = out + ((size_t)b * e + i) * out_pitch;
+        // decode row i, source q (survivors ascending, then the parity rows)
+        auto dcoef = [&](int q, int i) -> uint8_t {
+            if (i >= e)
+                return 0;
+            if (q < nl) {
+                const uint8_t d = gexp[lv[q]] ^ aa[i];  // b_q + a_i, never 0
+                return gexp[(lb[q] + 2 * 255 - glog[d] - lw[i]) % 255];
+            }
+            return A[i * e + (q - nl)];
+        };
+        if (jit_code) {
+            // k_rs_jit's code (rs_jit.h): item (w, q) writes source q's part
+            // of wave w's chunk q / 8; items (w, ch) the chunk's ends
+            const int NW = (e + 7) / 8, nch = (k + 7) / 8;
+            const size_t stride = (size_t)jit::chunk_stride(8);
+            uint8_t* cb = jit_code + (size_t)b * NW * nch * stride;
+            for (int idx = tid; idx < NW * k; idx += nt) {
+                const int w = idx / k, q = idx - w * k;
+                const int ch = q / 8, t = q - 8 * ch, ntc = min(8, k - 8 * ch);
+                const int nslot = min(8, e - 8 * w);
+                uint64_t* dst = reinterpret_cast<uint64_t*>(cb + ((size_t)w * nch + ch) * stride +
+                                                            jit::PRO_BYTES +
+                                                            (size_t)t * jit::src_bytes(nslot));
+                jit::emit_pre(dst, t, ntc);
+                for (int s = 0; s < nslot; ++s)
+                    jit::emit_mac(dst + jit::PRE_BYTES / 8 + 8 * s, dcoef(q, 8 * w + s), s, t & 1);
+            }
+            for (int idx = tid; idx < NW * nch; idx += nt) {
+                const int w = idx / nch, ch = idx - w * nch, ntc = min(8, k - 8 * ch);
+                const int nslot = min(8, e - 8 * w);
+                uint8_t* base = cb + ((size_t)w * nch + ch) * stride;
+                jit::emit_prologue(reinterpret_cast<uint64_t*>(base));
+                jit::emit_epilogue(reinterpret_cast<uint64_t*>(
+                    base + jit::PRO_BYTES + (size_t)ntc * jit::src_bytes(nslot)));
+            }
+            return;
+        }
         unsigned long long* da = dir_addr + (size_t)b * k * tc_rows;
         for (int idx = tid; idx < k * tc_rows; idx += nt) {
             const int q = idx / tc_rows, i = idx - q * tc_rows;
-            uint8_t c = 0;
-            if (i < e) {
-                if (q < nl) {
-                    const uint8_t d = gexp[lv[q]] ^ aa[i];  // b_q + a_i, never 0
-                    c = gexp[(lb[q] + 2 * 255 - glog[d] - lw[i]) % 255];
-                } else {
-                    c = A[i * e + (q - nl)];
-                }
-            }
-            da[idx] = tc_table[(i & 7) * 256 + c];
+            da[idx] = tc_table[(i & 7) * 256 + dcoef(q, i)];
         }
         return;
     }
@@ -1120,9 +1150,11 @@ hipError_t launch_decode_prepare_syn(int k, int e, long long blocks, const uint8
                                      unsigned long long* tc_addr, unsigned long long* emask,
                                      int* status, unsigned long long* syn_addr,
                                      const uint8_t* src, const uint8_t* par,
-                                     unsigned long long* dir_addr, hipStream_t st)
+                                     unsigned long long* dir_addr, uint8_t* jit_code,
+                                     hipStream_t st)
 {
-    if (k <= 0 || k > 250 || e <= 0 || e > 32 || !tc_table || (!dir_addr && (!tc_addr || !syn_addr)))
+    if (k <= 0 || k > 250 || e <= 0 || e > 32 ||
+        (!jit_code && (!tc_table || (!dir_addr && (!tc_addr || !syn_addr)))))
         return hipErrorInvalidValue;
     static bool attr_set = false;
     if (!attr_set) {
@@ -1132,7 +1164,7 @@ hipError_t launch_decode_prepare_syn(int k, int e, long long blocks, const uint8
     }
     hipLaunchKernelGGL(k_decode_prepare_syn, dim3((unsigned)blocks), dim3(256),
                        decode_prepare_syn_lds_bytes(e), st, k, e, err, out, out_pitch, srcs, dsts,
-                       tc_table, tc_addr, emask, status, syn_addr, src, par, dir_addr);
+                       tc_table, tc_addr, emask, status, syn_addr, src, par, dir_addr, jit_code);
     return hipGetLastError();
 }
 

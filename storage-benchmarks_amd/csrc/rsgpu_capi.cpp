@@ -2,6 +2,8 @@
 // ISA-L semantics, context/stream management, and the launch sequences of the
 // batched encode / decode hot path.
 #include <hip/hip_runtime.h>
+#include <hsa/hsa.h>
+#include <hsa/hsa_ext_amd.h>
 
 #include <algorithm>
 #include <cstdio>
@@ -12,6 +14,7 @@
 
 #include "../../include/rsgpu.h"
 #include "gf256.h"
+#include "rs_jit.h"
 #include "rs_kernels.h"
 #include "rs_synth.h"
 
@@ -28,6 +31,12 @@ struct rsgpu_ctx {
     unsigned long long h_tc_table[2048] = {};
     int tc_state = 0;
     int decode_kernel = RSGPU_DECODE_AUTO;
+    // executable device memory for the generated decode code (rs_jit.h):
+    // grow-only; jit_state 0 = not probed, 1 = pool found, -1 = unavailable
+    void* d_jit = nullptr;
+    size_t jit_bytes = 0;
+    int jit_state = 0;
+    hsa_amd_memory_pool_t jit_pool{};
     std::string err;
     // grow-only device scratch for pointer tables / coefficient tables
     void* d_scratch = nullptr;
@@ -229,6 +238,76 @@ int tc_init(rsgpu_ctx* ctx)
 
 bool tc_ready(rsgpu_ctx* ctx) { return tc_init(ctx) == 1; }
 
+hsa_status_t pick_coarse_pool(hsa_amd_memory_pool_t p, void* out)
+{
+    hsa_amd_segment_t seg;
+    if (hsa_amd_memory_pool_get_info(p, HSA_AMD_MEMORY_POOL_INFO_SEGMENT, &seg) != HSA_STATUS_SUCCESS ||
+        seg != HSA_AMD_SEGMENT_GLOBAL)
+        return HSA_STATUS_SUCCESS;
+    uint32_t flags = 0;
+    bool alloc = false;
+    hsa_amd_memory_pool_get_info(p, HSA_AMD_MEMORY_POOL_INFO_GLOBAL_FLAGS, &flags);
+    hsa_amd_memory_pool_get_info(p, HSA_AMD_MEMORY_POOL_INFO_RUNTIME_ALLOC_ALLOWED, &alloc);
+    if ((flags & HSA_AMD_MEMORY_POOL_GLOBAL_FLAG_COARSE_GRAINED) && alloc) {
+        *(hsa_amd_memory_pool_t*)out = p;
+        return HSA_STATUS_INFO_BREAK;
+    }
+    return HSA_STATUS_SUCCESS;
+}
+
+// The device's coarse-grained pool, found through the owner of a hipMalloc'd
+// probe (the HSA agent behind this HIP device): executable allocations for
+// the generated decode code come from it.
+int jit_probe(rsgpu_ctx* ctx)
+{
+    if (ctx->jit_state != 0)
+        return ctx->jit_state;
+    ctx->jit_state = -1;
+    void* probe = nullptr;
+    if (hipMalloc(&probe, 256) != hipSuccess)
+        return -1;
+    hsa_amd_pointer_info_t info{};
+    info.size = sizeof(info);
+    const bool ok = hsa_amd_pointer_info(probe, &info, nullptr, nullptr, nullptr) == HSA_STATUS_SUCCESS;
+    (void)hipFree(probe);
+    if (!ok)
+        return -1;
+    hsa_amd_memory_pool_t pool{};
+    pool.handle = 0;
+    hsa_amd_agent_iterate_memory_pools(info.agentOwner, pick_coarse_pool, &pool);
+    if (!pool.handle)
+        return -1;
+    ctx->jit_pool = pool;
+    ctx->jit_state = 1;
+    return 1;
+}
+
+// >= bytes of executable device memory, filled with returns when (re)made.
+// Every kernel that may still execute the old code was enqueued on the
+// context stream (or one it waits on): synchronising it retires them.
+int jit_ensure(rsgpu_ctx* ctx, size_t bytes)
+{
+    if (ctx->jit_bytes >= bytes)
+        return RSGPU_OK;
+    if (jit_probe(ctx) != 1)
+        return fail(ctx, RSGPU_ERR_UNSUPPORTED, "no executable device memory pool");
+    if (ctx->d_jit) {
+        RS_HIP(ctx, hipStreamSynchronize(ctx->stream));
+        hsa_amd_memory_pool_free(ctx->d_jit);
+        ctx->d_jit = nullptr;
+        ctx->jit_bytes = 0;
+    }
+    const size_t want = std::max<size_t>(bytes, 1u << 20);
+    void* p = nullptr;
+    if (hsa_amd_memory_pool_allocate(ctx->jit_pool, want, HSA_AMD_MEMORY_POOL_EXECUTABLE_FLAG, &p) !=
+            HSA_STATUS_SUCCESS || !p)
+        return fail(ctx, RSGPU_ERR_NOMEM, "executable device allocation failed");
+    ctx->d_jit = p;
+    ctx->jit_bytes = want;
+    RS_HIP(ctx, launch_jit_fill(p, want, ctx->stream));
+    return RSGPU_OK;
+}
+
 // Host-side handler addresses of coefficient matrix coef[rows][k] in the
 // pass layout (rs_kernels.h tc_elem): pass p, source j, slot s -> row 32p + s.
 void tc_fill_addr(const rsgpu_ctx* ctx, const uint8_t* coef, int k, int rows, unsigned long long* h)
@@ -398,6 +477,8 @@ int rsgpu_destroy(rsgpu_ctx* ctx)
         (void)hipEventDestroy(e);
     if (ctx->d_tc_table)
         (void)hipFree(ctx->d_tc_table);
+    if (ctx->d_jit)
+        hsa_amd_memory_pool_free(ctx->d_jit);
     delete ctx;
     return RSGPU_OK;
 }
@@ -727,7 +808,7 @@ int rsgpu_encode_blocks(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch, 
 
 int rsgpu_set_decode_kernel(rsgpu_ctx* ctx, int kernel)
 {
-    if (!ctx || kernel < RSGPU_DECODE_AUTO || kernel > RSGPU_DECODE_GENERAL)
+    if (!ctx || kernel < RSGPU_DECODE_AUTO || kernel > RSGPU_DECODE_GENERATED)
         return fail(ctx, RSGPU_ERR_ARG, "rsgpu_set_decode_kernel: unknown kernel");
     ctx->decode_kernel = kernel;
     return RSGPU_OK;
@@ -740,6 +821,7 @@ namespace {
 // How rsgpu_decode_blocks runs for a geometry (prepare and apply agree as
 // long as the context's decode kernel setting does not change in between).
 enum class Plan {
+    generated,   // k_decode_prepare_syn (closed form, writes code) + k_rs_jit
     one_matrix,  // k_decode_prepare_syn (closed form) + k_rs_tc
     fused,       // k_decode_prepare_syn (e x e) + k_rs_decode_fused
     general_tc,  // k_decode_prepare (k x k inversion) + k_rs_tc passes
@@ -760,11 +842,11 @@ Plan decode_plan(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch, const v
     const int want = ctx->decode_kernel;
     if (want == RSGPU_DECODE_GENERAL || e > 32)
         return Plan::general_tc;
-    // the fused kernel measured 3 % faster at (k 100, e 20) only
-    if (rs_decode_fused_available(k, e) &&
-        (want == RSGPU_DECODE_FUSED || (want == RSGPU_DECODE_AUTO && k == 100 && e == 20)))
+    if (want == RSGPU_DECODE_FUSED && rs_decode_fused_available(k, e))
         return Plan::fused;
-    return Plan::one_matrix;
+    if (want == RSGPU_DECODE_ONE_MATRIX || jit_probe(ctx) != 1)
+        return Plan::one_matrix;
+    return Plan::generated;  // AUTO / GENERATED
 }
 
 // Workspace: [emask B x 16 B | survivor ptrs B x k | output ptrs B x e |
@@ -889,17 +971,24 @@ int rsgpu_decode_prepare(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch,
     if (e > k || !d_err || !d_workspace || !d_status)
         return fail(ctx, RSGPU_ERR_ARG, "rsgpu_decode_prepare: bad arguments");
     const Plan plan = decode_plan(ctx, k, e, len, pitch, d_src, d_parity, d_out);
-    if (plan == Plan::one_matrix || plan == Plan::fused) {
+    if (plan == Plan::one_matrix || plan == Plan::fused || plan == Plan::generated) {
         const WsLayout w = ws_layout(k, e, blocks);
         char* ws = (char*)d_workspace;
-        const bool one = plan == Plan::one_matrix;
+        const bool one = plan == Plan::one_matrix, gen = plan == Plan::generated;
+        if (gen) {
+            rc = jit_ensure(ctx, jit_code_bytes(k, e, (long long)blocks));
+            if (rc)
+                return rc;
+        }
         KTimer kt(ctx, "k_decode_prepare_syn", blocks);
         RS_HIP(ctx, launch_decode_prepare_syn(
                         k, e, (long long)blocks, d_err, d_out, (long long)pitch,
                         (const uint8_t**)(ws + w.surv), (uint8_t**)(ws + w.outp), ctx->d_tc_table,
-                        one ? nullptr : (unsigned long long*)(ws + w.tab), (unsigned long long*)ws,
-                        d_status, one ? nullptr : (unsigned long long*)(ws + w.tab2), d_src, d_parity,
-                        one ? (unsigned long long*)(ws + w.tab) : nullptr, ctx->stream));
+                        plan == Plan::fused ? (unsigned long long*)(ws + w.tab) : nullptr,
+                        (unsigned long long*)ws, d_status,
+                        plan == Plan::fused ? (unsigned long long*)(ws + w.tab2) : nullptr, d_src,
+                        d_parity, one ? (unsigned long long*)(ws + w.tab) : nullptr,
+                        gen ? (uint8_t*)ctx->d_jit : nullptr, ctx->stream));
         return RSGPU_OK;
     }
     return general_prepare(ctx, plan, k, k + e, e, true, pitch, blocks, nullptr, d_src, d_parity,
@@ -920,6 +1009,23 @@ int rsgpu_decode_apply(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch, s
     const Plan plan = decode_plan(ctx, k, e, len, pitch, d_src, d_parity, d_out);
     const WsLayout w = ws_layout(k, e, blocks);
     char* ws = (char*)d_workspace;
+    if (plan == Plan::generated) {
+        // one pass, one matrix, the block's generated code (rs_jit.hip)
+        if (!ctx->d_jit || ctx->jit_bytes < jit_code_bytes(k, e, (long long)blocks))
+            return fail(ctx, RSGPU_ERR_ARG, "rsgpu_decode_apply: no prepared decode code");
+        JitArgs j{};
+        j.srcs = (const uint8_t* const*)(ws + w.surv);
+        j.dsts = (uint8_t* const*)(ws + w.outp);
+        j.code = (const uint8_t*)ctx->d_jit;
+        j.chunk_stride = jit::chunk_stride(8);
+        j.k = k;
+        j.rows = e;
+        j.len = (long long)len;
+        j.status = d_status;
+        KTimer kt(ctx, "k_rs_jit(decode)", blocks);
+        RS_HIP(ctx, launch_rs_jit(j, (long long)blocks, ctx->stream));
+        return RSGPU_OK;
+    }
     if (plan == Plan::one_matrix)
         // one pass, one matrix over the k - e survivors and the e parity rows
         return tc_launch(ctx, "k_rs_tc(decode)", (const uint8_t* const*)(ws + w.surv),
@@ -1026,6 +1132,45 @@ int rsgpu_fill_synthetic(rsgpu_ctx* ctx, unsigned char* d_rows, size_t rows, siz
     RS_HIP(ctx, launch_fill_synth(d_rows, (long long)rows, (long long)len, (long long)pitch, seed,
                                   row0, ctx->stream));
     return RSGPU_OK;
+}
+
+// Test hook (not part of include/rsgpu.h): the generated decode code of ONE
+// block for coefficient matrix coef[e][k], written on the host by the same
+// emitters the prepare kernel runs (rs_jit.h), so the CPU suite can
+// disassemble and interpret it.  Returns the bytes needed (jit_code_bytes)
+// or -1 for bad arguments; writes only when out_bytes is large enough.
+long long rsgpu_internal_jit_emit(int k, int e, const unsigned char* coef, unsigned char* out,
+                                  size_t out_bytes)
+{
+    if (k <= 0 || e <= 0 || e > 32 || !coef)
+        return -1;
+    const size_t need = jit_code_bytes(k, e, 1);
+    if (!out || out_bytes < need)
+        return (long long)need;
+    const int NW = (e + 7) / 8, nch = (k + 7) / 8;
+    const size_t stride = (size_t)jit::chunk_stride(8);
+    for (size_t i = 0; i < need / 8; ++i)
+        reinterpret_cast<uint64_t*>(out)[i] = (uint64_t)jit::S_NOP0 << 32 | jit::S_SETPC_82;
+    for (int w = 0; w < NW; ++w)
+        for (int q = 0; q < k; ++q) {
+            const int ch = q / 8, t = q - 8 * ch, ntc = std::min(8, k - 8 * ch);
+            const int nslot = std::min(8, e - 8 * w);
+            uint64_t* dst = reinterpret_cast<uint64_t*>(out + ((size_t)w * nch + ch) * stride +
+                                                        jit::PRO_BYTES + (size_t)t * jit::src_bytes(nslot));
+            jit::emit_pre(dst, t, ntc);
+            for (int s = 0; s < nslot; ++s)
+                jit::emit_mac(dst + jit::PRE_BYTES / 8 + 8 * s, coef[(size_t)(8 * w + s) * k + q], s,
+                              t & 1);
+        }
+    for (int w = 0; w < NW; ++w)
+        for (int ch = 0; ch < nch; ++ch) {
+            const int ntc = std::min(8, k - 8 * ch), nslot = std::min(8, e - 8 * w);
+            unsigned char* base = out + ((size_t)w * nch + ch) * stride;
+            jit::emit_prologue(reinterpret_cast<uint64_t*>(base));
+            jit::emit_epilogue(reinterpret_cast<uint64_t*>(base + jit::PRO_BYTES +
+                                                           (size_t)ntc * jit::src_bytes(nslot)));
+        }
+    return (long long)need;
 }
 
 int rsgpu_erasure_patterns(uint64_t seed, uint64_t blk0, size_t blocks, int k, int e,

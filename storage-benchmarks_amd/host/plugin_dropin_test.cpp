@@ -5,8 +5,8 @@
 // goodput accounting (:37-67), for the configurations given on the command
 // line as  symbols:symbol_size:erased ...
 //
-//   --decode-kernel K   rsgpu_set_decode_kernel: auto | one_matrix | fused |
-//                       general
+//   --decode-kernel K   rsgpu_set_decode_kernel: auto | generated |
+//                       one_matrix | fused | general
 //   --poison            after encode_all, overwrite every erased original row
 //                       on the device with 0xA5 (keeping a host copy): the
 //                       reference's decoder never reads them (isa.cpp:193-
@@ -104,6 +104,7 @@ int main(int argc, char** argv)
             kernel = k == "one_matrix" ? RSGPU_DECODE_ONE_MATRIX
                    : k == "fused"      ? RSGPU_DECODE_FUSED
                    : k == "general"    ? RSGPU_DECODE_GENERAL
+                   : k == "generated"  ? RSGPU_DECODE_GENERATED
                                        : RSGPU_DECODE_AUTO;
         } else {
             cfgs.push_back(a);

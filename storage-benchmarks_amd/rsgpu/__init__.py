@@ -46,7 +46,7 @@ ERRORS = {-1: "RSGPU_ERR_ARG", -2: "RSGPU_ERR_HIP", -3: "RSGPU_ERR_SINGULAR",
           -4: "RSGPU_ERR_NOMEM", -5: "RSGPU_ERR_UNSUPPORTED"}
 MAX_SOURCES = 250  # TEST_SOURCES, isa.cpp:25-27
 # rsgpu_set_decode_kernel choices (include/rsgpu.h)
-DECODE_KERNELS = {"auto": 0, "one_matrix": 1, "fused": 2, "general": 3}
+DECODE_KERNELS = {"auto": 0, "one_matrix": 1, "fused": 2, "general": 3, "generated": 4}
 
 vp = C.c_void_p
 sz = C.c_size_t

@@ -28,7 +28,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 GOLD = json.load(open(os.path.join(HERE, "golden", "golden.json")))
 BIN = os.path.join(ROOT, "storage-benchmarks_amd", "bin")
-KERNELS = ["auto", "one_matrix", "fused", "general"]
+KERNELS = ["auto", "generated", "one_matrix", "fused", "general"]
 
 
 def sha(b):

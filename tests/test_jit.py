@@ -1,0 +1,156 @@
+"""The generated decode code (storage-benchmarks_amd/csrc/rs_jit.h) checked on
+the CPU: librsgpu's host emitter (the same functions the prepare kernel runs on
+the GPU) writes one block's code, llvm-mc disassembles it, and an interpreter
+runs it with LDS-resident bit planes.  Every accumulator must end as
+sum_q c[row][q] * src_q over GF(2^8) (isa/ec_base.c:36-48 gf_mul), only the
+allowed instructions may appear, the layout must not depend on the
+coefficients, and no register may be read while an LDS load into it is
+still outstanding."""
+import ctypes as C
+import os
+import random
+import re
+import shutil
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(os.path.dirname(HERE), "storage-benchmarks_amd", "csrc"))
+import gen_tc_handlers as g  # noqa: E402
+from test_codegen import planes, unplanes  # noqa: E402
+
+LLVM_MC = shutil.which("llvm-mc") or "/opt/rocm/lib/llvm/bin/llvm-mc"
+pytestmark = pytest.mark.skipif(not os.path.exists(LLVM_MC), reason="llvm-mc not available")
+
+ALLOWED = {"v_bitop3_b32", "v_xor_b32_e32", "v_xor_b32_e64", "ds_read_b128", "s_waitcnt", "s_nop",
+           "s_setpc_b64"}
+CHUNK_STRIDE = 5056  # jit::chunk_stride(8): (16 + 8 * 624 + 8) rounded to 64
+
+
+def emit(k, e, coef):
+    import rsgpu
+    f = rsgpu.lib().rsgpu_internal_jit_emit
+    f.restype = C.c_longlong
+    f.argtypes = [C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_size_t]
+    coef = np.ascontiguousarray(coef, np.uint8)
+    need = f(k, e, coef.ctypes.data, None, 0)
+    out = np.zeros(need, np.uint8)
+    assert f(k, e, coef.ctypes.data, out.ctypes.data, need) == need
+    return out
+
+
+def disasm(code: bytes):
+    """[(byte offset, mnemonic, operand text)] via llvm-mc, instruction sizes
+    from the encodings (VOP3 / DS: 8 bytes, SOPP / SOP1 / VOP2: 4)."""
+    text = " ".join(f"0x{b:02x}" for b in code)
+    r = subprocess.run([LLVM_MC, "-arch=amdgcn", "-mcpu=gfx950", "--disassemble", "-show-encoding"],
+                       input=text, capture_output=True, text=True, check=True)
+    out, off = [], 0
+    for ln in r.stdout.splitlines():
+        ln = ln.strip()
+        if not ln or ln.startswith("."):
+            continue
+        body, _, enc = ln.partition(";")
+        n = enc.count("0x")
+        assert n in (4, 8), ln
+        mnem, _, ops = body.strip().partition(" ")
+        out.append((off, mnem, ops.strip()))
+        off += n
+    assert off == len(code), (off, len(code))
+    return out
+
+
+def regs_of(op):
+    m = re.fullmatch(r"v\[(\d+):(\d+)\]", op)
+    if m:
+        return list(range(int(m.group(1)), int(m.group(2)) + 1))
+    return [int(op[1:])]
+
+
+def run_chunk(ins, regs, lds, pending):
+    """Interpret one chunk up to its s_setpc; LDS loads land at issue but stay
+    'pending' until an s_waitcnt retires them (reading one is a hazard)."""
+    def rd(r):
+        for p in pending:
+            assert r not in p, f"v{r} read before its LDS load was waited for"
+        return regs[r]
+
+    for off, mnem, ops in ins:
+        assert mnem in ALLOWED, mnem
+        a = [x.strip() for x in ops.split(",")] if ops else []
+        if mnem == "s_setpc_b64":
+            return off
+        if mnem == "s_nop":
+            continue
+        if mnem == "s_waitcnt":
+            n = int(re.fullmatch(r"lgkmcnt\((\d+)\)", ops).group(1))
+            del pending[: max(0, len(pending) - n)]
+        elif mnem == "ds_read_b128":
+            dst = regs_of(a[0])
+            addr, _, rest = a[1].partition(" ")
+            assert addr == "v20", ops
+            o = int(rest.split(":")[1]) if rest else 0
+            for i, r in enumerate(dst):
+                regs[r] = lds[o + 4 * i]
+            pending.append(set(dst))
+        elif mnem.startswith("v_xor"):
+            d, x, y = (regs_of(v)[0] for v in a)
+            regs[d] = rd(x) ^ rd(y)
+        elif mnem == "v_bitop3_b32":
+            last, _, mod = a[3].partition(" ")
+            assert mod == "bitop3:0x96", ops
+            d, x, y, z = (regs_of(v)[0] for v in a[:3] + [last])
+            regs[d] = rd(x) ^ rd(y) ^ rd(z)
+    raise AssertionError("chunk without a return")
+
+
+@pytest.mark.parametrize("k,e", [(64, 32), (20, 13), (9, 8), (100, 20), (3, 1)])
+def test_generated_block_decodes(k, e):
+    rng = random.Random(k * 100 + e)
+    coef = np.array([[rng.randrange(256) for _ in range(k)] for _ in range(e)], np.uint8)
+    coef[0, 0] = 0  # a zero coefficient: no-op rows
+    code = emit(k, e, coef).tobytes()
+    nw, nch = (e + 7) // 8, (k + 7) // 8
+    assert len(code) == nw * nch * CHUNK_STRIDE
+    src = [[rng.randrange(256) for _ in range(32)] for _ in range(k)]
+    for w in range(nw):
+        regs = {r: 0 for r in range(256)}
+        pending = []
+        for ch in range(nch):
+            base = (w * nch + ch) * CHUNK_STRIDE
+            nt = min(8, k - 8 * ch)
+            nslot = min(8, e - 8 * w)
+            end = base + 16 + nt * (112 + 64 * nslot)
+            ins = disasm(code[base:end + 4])
+            lds = {}
+            for t in range(nt):
+                p = planes(src[8 * ch + t])
+                for a in range(8):
+                    lds[t * 2048 + (a // 4) * 1024 + 4 * (a % 4)] = p[a]
+            ret = run_chunk(ins, regs, lds, pending)
+            assert base + ret == end, "the return sits right after the last source"
+            assert not pending, "a load left outstanding at the return"
+        for s in range(min(8, e - 8 * w)):
+            row = 8 * w + s
+            want = [0] * 32
+            for q in range(k):
+                want = [x ^ g.gf_mul(int(coef[row, q]), y) for x, y in zip(want, src[q])]
+            got = unplanes([regs[64 + 8 * s + b] for b in range(8)])
+            assert got == want, (k, e, row)
+
+
+def test_layout_independent_of_coefficients():
+    """Instruction boundaries and kinds depend on (k, e) only: a block's code
+    rewritten with other coefficients never puts an instruction boundary
+    elsewhere (what a stale instruction-cache line would otherwise expose)."""
+    k, e = 24, 17
+    rng = np.random.default_rng(5)
+    layouts = []
+    for _ in range(3):
+        coef = rng.integers(1, 256, (e, k), dtype=np.uint8)
+        ins = disasm(emit(k, e, coef).tobytes())
+        layouts.append([(off, m.startswith("v_") and m != "ds_read_b128") for off, m, _ in ins])
+    assert layouts[0] == layouts[1] == layouts[2]
