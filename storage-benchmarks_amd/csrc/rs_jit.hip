@@ -39,6 +39,35 @@ using bs::wait_vm;
 
 constexpr int C = 8;  // sources per LDS chunk (double-buffered)
 
+// Phase accounting for tools/jit_profile.hip (compiled in only there, with
+// -DRSGPU_JIT_PROF): per-wave s_memtime sums of each phase, sampled
+// workgroups, added into rsgpu_jit_prof[phase] at the end of the wave.
+#ifdef RSGPU_JIT_PROF
+__device__ unsigned long long rsgpu_jit_prof[8];
+#define JP_DECL unsigned long long jp_sum[8] = {}, jp_t = __builtin_amdgcn_s_memtime(), jp_start = jp_t;
+#define JP_MARK(P)                                                     \
+    do {                                                               \
+        const unsigned long long jp_n = __builtin_amdgcn_s_memtime();  \
+        jp_sum[P] += jp_n - jp_t;                                      \
+        jp_t = jp_n;                                                   \
+    } while (0)
+#define JP_END                                                                          \
+    do {                                                                                \
+        jp_sum[7] = __builtin_amdgcn_s_memtime() - jp_start;                            \
+        if (lane == 0 && (blockIdx.x & 63) == 0)                                        \
+            for (int i = 0; i < 8; ++i)                                                 \
+                atomicAdd(&rsgpu_jit_prof[i], jp_sum[i]);                               \
+    } while (0)
+#else
+#define JP_DECL
+#define JP_MARK(P) \
+    do {           \
+    } while (0)
+#define JP_END \
+    do {       \
+    } while (0)
+#endif
+
 template <int S>
 __device__ __forceinline__ void read_slot(uint32_t (&W)[8])
 {
@@ -63,6 +92,11 @@ __device__ __forceinline__ void read_slot(uint32_t (&W)[8])
 // amdgpu_num_vgpr(64): the compiler allocates v0..v63 only (minus the
 // registers the call clobbers); the accumulators v64..v127 are touched by asm
 // and generated code alone.
+// amdgpu_num_vgpr(64): the compiler allocates v0..v63 only (minus the
+// registers the call clobbers); the accumulators v64..v127 are touched by asm
+// and generated code alone.  (Holding the block's row pointers in VGPRs and
+// reading them with v_readlane instead of scalar loads measured slower:
+// 26.3 vs 25.1 ms at C3, tools/jit_profile.)
 template <int NW>
 __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_num_vgpr(64))) void k_rs_jit(JitArgs a)
 {
@@ -86,6 +120,8 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_num_vgpr(64))) void 
 
     asm volatile("s_icache_inv\n s_nop 15\n s_nop 15" ::: "memory");
 
+    // chunk ch's sources this wave moves: t = wave, wave + NW, ... (two row
+    // pointers per scalar wait)
     auto issue = [&](int ch) {
         const int c0 = ch * C, nt = min(C, k - c0);
         const uint32_t base = lds0 + (uint32_t)((ch & 1) * C * 2 * 64 * 16);
@@ -104,13 +140,31 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_num_vgpr(64))) void 
     };
 
     asm volatile(RSGPU_TC_ZERO ::: RSGPU_TC_ACC_CLOBBERS);
+    JP_DECL
     issue(0);
+    JP_MARK(3);
     for (int ch = 0; ch < nch; ++ch) {
         const int nt = min(C, k - ch * C);
         uint4* buf = lds[ch & 1];
         wait_vm(0);  // this chunk's own sources, issued behind the previous barrier
-        // own share of this chunk: bytes -> bit-planes, in place
-        for (int t = wave; t < nt; t += NW) {
+        JP_MARK(0);
+        // own share of this chunk: bytes -> bit-planes, in place, two
+        // sources at a time (both sets of LDS reads in flight together)
+        int t = wave;
+        for (; t + NW < nt; t += 2 * NW) {
+            const int t1 = t + NW;
+            uint4 u0 = buf[(t * 2 + 0) * 64 + lane], v0 = buf[(t * 2 + 1) * 64 + lane];
+            uint4 u1 = buf[(t1 * 2 + 0) * 64 + lane], v1 = buf[(t1 * 2 + 1) * 64 + lane];
+            uint32_t W0[8] = {u0.x, u0.y, u0.z, u0.w, v0.x, v0.y, v0.z, v0.w};
+            uint32_t W1[8] = {u1.x, u1.y, u1.z, u1.w, v1.x, v1.y, v1.z, v1.w};
+            tr8(W0, m4, m2, m1);
+            tr8(W1, m4, m2, m1);
+            buf[(t * 2 + 0) * 64 + lane] = make_uint4(W0[0], W0[1], W0[2], W0[3]);
+            buf[(t * 2 + 1) * 64 + lane] = make_uint4(W0[4], W0[5], W0[6], W0[7]);
+            buf[(t1 * 2 + 0) * 64 + lane] = make_uint4(W1[0], W1[1], W1[2], W1[3]);
+            buf[(t1 * 2 + 1) * 64 + lane] = make_uint4(W1[4], W1[5], W1[6], W1[7]);
+        }
+        if (t < nt) {
             uint4 u = buf[(t * 2 + 0) * 64 + lane];
             uint4 v = buf[(t * 2 + 1) * 64 + lane];
             uint32_t W[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
@@ -118,11 +172,14 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_num_vgpr(64))) void 
             buf[(t * 2 + 0) * 64 + lane] = make_uint4(W[0], W[1], W[2], W[3]);
             buf[(t * 2 + 1) * 64 + lane] = make_uint4(W[4], W[5], W[6], W[7]);
         }
+        JP_MARK(1);
         barrier_lds();
+        JP_MARK(2);
         // one barrier per chunk: every wave is past its call of chunk ch - 1,
         // which read buffer (ch + 1) & 1, so chunk ch + 1 may land there now
         if (ch + 1 < nch)
             issue(ch + 1);
+        JP_MARK(3);
         const uint32_t la = lds0 + (uint32_t)((ch & 1) * C * 2 * 64 * 16) + lane * 16;
         const uint8_t* fn = code + (size_t)ch * a.chunk_stride;
         asm volatile("s_swappc_b64 s[82:83], %[fn]"
@@ -133,6 +190,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_num_vgpr(64))) void 
                        "v46", "v47", "v48", "v49", "v50", "v51", "v52", "v53", "v54", "v55", "v56",
                        "v57", "v58", "v59", "v60", "v61", "s82", "s83", "scc", "memory",
                        RSGPU_TC_ACC_CLOBBERS);
+        JP_MARK(4);
     }
     // outputs back to bytes and out (every source of this tile was read
     // before the last barrier)
@@ -151,6 +209,8 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_num_vgpr(64))) void 
                 ...);
         }(std::make_integer_sequence<int, 8>{});
     }
+    JP_MARK(5);
+    JP_END;
 }
 
 // every 8-byte slot a return: a call that lands in code never written

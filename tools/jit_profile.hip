@@ -1,0 +1,157 @@
+// jit_profile.hip -- where the waves of k_rs_jit spend their time (tool, not
+// product).  Compiles the kernel source with -DRSGPU_JIT_PROF (per-wave
+// s_memtime sums per phase), writes random-coefficient code for every block
+// with the host emitters of rs_jit.h, copies it into executable device
+// memory, runs the decode kernel on synthetic rows and prints the average
+// cycles per wave in each phase.
+//   make -C storage-benchmarks_amd build/tc_handlers.inc
+//   hipcc --offload-arch=gfx950 -O3 -std=c++20 -DRSGPU_JIT_PROF \
+//     -Istorage-benchmarks_amd/csrc -Istorage-benchmarks_amd/build \
+//     -o tools/jit_profile tools/jit_profile.hip -lhsa-runtime64
+//   tools/jit_profile [blocks=512] [k=64] [rows=32]
+#include "../storage-benchmarks_amd/csrc/rs_jit.hip"
+
+#include <hsa/hsa.h>
+#include <hsa/hsa_ext_amd.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <vector>
+
+static hsa_status_t pick(hsa_amd_memory_pool_t p, void* d)
+{
+    hsa_amd_segment_t seg;
+    hsa_amd_memory_pool_get_info(p, HSA_AMD_MEMORY_POOL_INFO_SEGMENT, &seg);
+    uint32_t flags = 0;
+    bool alloc = false;
+    hsa_amd_memory_pool_get_info(p, HSA_AMD_MEMORY_POOL_INFO_GLOBAL_FLAGS, &flags);
+    hsa_amd_memory_pool_get_info(p, HSA_AMD_MEMORY_POOL_INFO_RUNTIME_ALLOC_ALLOWED, &alloc);
+    if (seg == HSA_AMD_SEGMENT_GLOBAL && (flags & HSA_AMD_MEMORY_POOL_GLOBAL_FLAG_COARSE_GRAINED) && alloc) {
+        *(hsa_amd_memory_pool_t*)d = p;
+        return HSA_STATUS_INFO_BREAK;
+    }
+    return HSA_STATUS_SUCCESS;
+}
+
+__global__ void k_copy(uint64_t* dst, const uint64_t* src, long long n)
+{
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (long long)gridDim.x * blockDim.x)
+        dst[i] = src[i];
+}
+
+int main(int argc, char** argv)
+{
+    using namespace rsgpu;
+    const int B = argc > 1 ? atoi(argv[1]) : 512;
+    const int k = argc > 2 ? atoi(argv[2]) : 64;
+    const int e = argc > 3 ? atoi(argv[3]) : 32;
+    const long long L = 1000000, pitch = 1000192;
+    uint8_t* rows;
+    if (hipMalloc(&rows, (size_t)B * (k + e) * pitch) != hipSuccess) {
+        printf("alloc failed\n");
+        return 1;
+    }
+    (void)hipMemset(rows, 0x5A, (size_t)B * (k + e) * pitch);
+    std::vector<const uint8_t*> sp((size_t)B * k), dp((size_t)B * e);
+    for (int b = 0; b < B; ++b) {
+        for (int j = 0; j < k; ++j)
+            sp[(size_t)b * k + j] = rows + ((size_t)b * (k + e) + j) * pitch;
+        for (int i = 0; i < e; ++i)
+            dp[(size_t)b * e + i] = rows + ((size_t)b * (k + e) + k + i) * pitch;
+    }
+    const uint8_t** d_sp;
+    uint8_t** d_dp;
+    (void)hipMalloc(&d_sp, sp.size() * 8);
+    (void)hipMalloc(&d_dp, dp.size() * 8);
+    (void)hipMemcpy(d_sp, sp.data(), sp.size() * 8, hipMemcpyHostToDevice);
+    (void)hipMemcpy(d_dp, dp.data(), dp.size() * 8, hipMemcpyHostToDevice);
+    int* d_st;
+    (void)hipMalloc(&d_st, B * sizeof(int));
+    (void)hipMemset(d_st, 0, B * sizeof(int));
+
+    // random-coefficient code of every block, host-emitted
+    const size_t per = jit_code_bytes(k, e, 1);
+    std::vector<uint64_t> code(per / 8 * B);
+    const int NW = (e + 7) / 8, nch = (k + 7) / 8;
+    const size_t stride = (size_t)jit::chunk_stride(8);
+    uint32_t x = 12345;
+    for (int b = 0; b < B; ++b) {
+        uint8_t* cb = (uint8_t*)code.data() + (size_t)b * per;
+        for (size_t i = 0; i < per / 8; ++i)
+            ((uint64_t*)cb)[i] = (uint64_t)jit::S_NOP0 << 32 | jit::S_SETPC_82;
+        for (int w = 0; w < NW; ++w)
+            for (int q = 0; q < k; ++q) {
+                const int ch = q / 8, t = q - 8 * ch, ntc = std::min(8, k - 8 * ch);
+                const int nslot = std::min(8, e - 8 * w);
+                uint64_t* dst = (uint64_t*)(cb + ((size_t)w * nch + ch) * stride + jit::PRO_BYTES +
+                                            (size_t)t * jit::src_bytes(nslot));
+                jit::emit_pre(dst, t, ntc);
+                for (int s = 0; s < nslot; ++s) {
+                    x = x * 1664525u + 1013904223u;
+                    jit::emit_mac(dst + jit::PRE_BYTES / 8 + 8 * s, (uint8_t)(x >> 13), s, t & 1);
+                }
+            }
+        for (int w = 0; w < NW; ++w)
+            for (int ch = 0; ch < nch; ++ch) {
+                const int ntc = std::min(8, k - 8 * ch), nslot = std::min(8, e - 8 * w);
+                uint8_t* base = cb + ((size_t)w * nch + ch) * stride;
+                jit::emit_prologue((uint64_t*)base);
+                jit::emit_epilogue((uint64_t*)(base + jit::PRO_BYTES + (size_t)ntc * jit::src_bytes(nslot)));
+            }
+    }
+    uint64_t* d_stage;
+    (void)hipMalloc(&d_stage, code.size() * 8);
+    (void)hipMemcpy(d_stage, code.data(), code.size() * 8, hipMemcpyHostToDevice);
+    hsa_amd_pointer_info_t info{};
+    info.size = sizeof(info);
+    hsa_amd_pointer_info(d_stage, &info, nullptr, nullptr, nullptr);
+    hsa_amd_memory_pool_t pool{};
+    hsa_amd_agent_iterate_memory_pools(info.agentOwner, pick, &pool);
+    void* exec = nullptr;
+    if (hsa_amd_memory_pool_allocate(pool, code.size() * 8, HSA_AMD_MEMORY_POOL_EXECUTABLE_FLAG, &exec) !=
+        HSA_STATUS_SUCCESS) {
+        printf("exec alloc failed\n");
+        return 1;
+    }
+    hipLaunchKernelGGL(k_copy, dim3(4096), dim3(256), 0, 0, (uint64_t*)exec, d_stage, (long long)code.size());
+
+    JitArgs a{};
+    a.srcs = d_sp;
+    a.dsts = d_dp;
+    a.code = (const uint8_t*)exec;
+    a.chunk_stride = (long long)stride;
+    a.k = k;
+    a.rows = e;
+    a.len = L;
+    a.status = d_st;
+    for (int rep = 0; rep < 2; ++rep) {  // warm, then measured
+        unsigned long long z[8] = {};
+        (void)hipMemcpyToSymbol(HIP_SYMBOL(jitk::rsgpu_jit_prof), z, sizeof z);
+        hipEvent_t e0, e1;
+        (void)hipEventCreate(&e0);
+        (void)hipEventCreate(&e1);
+        (void)hipEventRecord(e0);
+        (void)launch_rs_jit(a, B, 0);
+        (void)hipEventRecord(e1);
+        if (hipDeviceSynchronize() != hipSuccess) {
+            printf("kernel failed\n");
+            return 1;
+        }
+        float ms = 0;
+        (void)hipEventElapsedTime(&ms, e0, e1);
+        unsigned long long p[8];
+        (void)hipMemcpyFromSymbol(p, HIP_SYMBOL(jitk::rsgpu_jit_prof), sizeof p);
+        const double waves = (double)p[7] > 0 ? 1 : 1;
+        (void)waves;
+        const char* names[8] = {"wait vmcnt (LDS-DMA)", "transpose in", "barrier",
+                                "issue DMA", "generated code", "store out", "-", "wave lifetime"};
+        const long long wg = ((L + 2047) / 2048 + 63) / 64 * (long long)B;  // sampled WGs ~ x & 63 == 0
+        printf("rep %d: %.3f ms for %d blocks (%.2f TB/s alg)\n", rep, ms, B,
+               (double)B * (k + e) * L / (ms * 1e-3) / 1e12);
+        for (int i = 0; i < 8; ++i)
+            printf("  %-22s %12.0f cycles per wave (%.1f %%)\n", names[i],
+                   (double)p[i] / (wg * NW), 100.0 * p[i] / p[7]);
+    }
+    return 0;
+}

@@ -7,10 +7,9 @@ from collections import defaultdict
 
 
 def short(k: str) -> str:
-    for key in ("k_rs_decode_fused", "k_rs_tc", "k_rs_bs", "k_dot_generic", "k_decode_prepare_syn", "k_fill_synth"):
+    for key in ("k_rs_decode_fused", "k_rs_tc", "k_rs_jit", "k_rs_bs", "k_dot_generic",
+                "k_decode_prepare_syn", "k_fill_synth"):
         if key in k:
-            if key == "k_rs_bs":
-                return "k_rs_bs(syndrome)" if k.split(">")[0].rstrip().endswith("true") else "k_rs_bs(encode)"
             return key
     return k.split("(")[0][:40]
 
