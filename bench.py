@@ -416,9 +416,10 @@ def run_streamed(args, rsgpu, ctx, dev, rank, world, k, e, L, total_blocks):
     resident batches.  Per batch: sources generated on the device and the
     erasure lists (global block index) uploaded on the `gen` stream; encode +
     decode (the timed regions, HIP events) and the device verify on the
-    compute stream; batch i+1's generation overlaps batch i's compute.
-    Returns (timed seconds, wall seconds, mismatching bytes, batches, kernel
-    records)."""
+    compute stream.
+    Batch i+1's generation waits for batch i's decode, so it overlaps only
+    the verification and the timed kernels run alone.  Returns (timed
+    seconds, wall seconds, mismatching bytes, batches, kernel records)."""
     import numpy as np
     import torch
     share = total_blocks // world
@@ -450,6 +451,10 @@ def run_streamed(args, rsgpu, ctx, dev, rank, world, k, e, L, total_blocks):
             ev_gen[i - 2].synchronize()  # its upload from this pinned buffer is done
         h_err[i & 1][:nb] = torch.from_numpy(rsgpu.erasure_patterns(args.seed, b0, nb, k, e))
         with torch.cuda.stream(s_gen):
+            if i >= 1:
+                # after batch i-1's decode: generation overlaps only its
+                # verification, never the timed encode / decode kernels
+                s_gen.wait_event(ev_t[i - 1][1])
             if i >= 2:
                 s_gen.wait_event(ev_done[i - 2])  # batch i-2 (same buffers) verified
             gen_ctx.fill_synthetic(enc.src, nb * k, L, enc.pitch, args.seed, b0 * k)
@@ -467,14 +472,14 @@ def run_streamed(args, rsgpu, ctx, dev, rank, world, k, e, L, total_blocks):
     for i in range(nb_total):
         enc, dec = sets[i & 1]
         nb = min(batch, share - i * batch)
-        if i + 1 < nb_total:
-            generate(i + 1)
         s_cmp.wait_event(ev_gen[i])
         ev_t[i][0].record(s_cmp)
         ctx.encode_blocks(k, e, L, enc.pitch, nb, enc.src, enc.par)
         ctx.decode_blocks(k, e, L, enc.pitch, nb, enc.src, enc.par, dec.err, dec.out, dec.ws,
                           dec.status)
         ev_t[i][1].record(s_cmp)
+        if i + 1 < nb_total:
+            generate(i + 1)
         if not args.no_verify:
             ctx.verify_blocks(k, e, L, enc.pitch, nb, enc.src, dec.out, dec.err, dec.mism)
             # fold this batch's mismatches (and failed blocks) into its slot

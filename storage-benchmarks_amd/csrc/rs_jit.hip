@@ -91,9 +91,6 @@ __device__ __forceinline__ void read_slot(uint32_t (&W)[8])
 
 // amdgpu_num_vgpr(64): the compiler allocates v0..v63 only (minus the
 // registers the call clobbers); the accumulators v64..v127 are touched by asm
-// and generated code alone.
-// amdgpu_num_vgpr(64): the compiler allocates v0..v63 only (minus the
-// registers the call clobbers); the accumulators v64..v127 are touched by asm
 // and generated code alone.  (Holding the block's row pointers in VGPRs and
 // reading them with v_readlane instead of scalar loads measured slower:
 // 26.3 vs 25.1 ms at C3, tools/jit_profile.)
@@ -112,7 +109,11 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_num_vgpr(64))) void 
     const uint8_t* const* srcs = a.srcs + (size_t)b * k;
     uint8_t* const* dsts = a.dsts + (size_t)b * a.rows;
     // this wave's generated code: chunk ch at code + ch * stride
+#ifndef RSGPU_JIT_SHARE
     const uint8_t* code = a.code + ((size_t)b * NW + wave) * (size_t)nch * a.chunk_stride;
+#else  // timing-only builds of tools/jit_profile: 1 = every wave runs wave 0's code, 2 = block 0's too
+    const uint8_t* code = a.code + (size_t)(RSGPU_JIT_SHARE == 2 ? 0 : b) * NW * (size_t)nch * a.chunk_stride;
+#endif
     const uint32_t m4 = vconst(0x0F0F0F0Fu), m2 = vconst(0x33333333u), m1 = vconst(0x55555555u);
     const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint4*)&lds[0][0];
     const long long off = tile * 2048 + lane * 32;
