@@ -64,11 +64,10 @@ RJ_HD constexpr int table_reg(int bank, int hi, int n)
         const int a = n == 1 ? 0 : n == 2 ? 1 : n == 4 ? 2 : 3;
         return plane_reg(bank, 4 * hi + a);
     }
-    // composites n = 3 5 6 7 9 10 11 12 13 14 15 -> 0..10
-    int idx = 0;
-    for (int m = 3; m < n; ++m)
-        idx += (m & (m - 1)) != 0;
-    return 32 + 11 * hi + idx;
+    // composites n = 3 5 6 7 9 10 11 12 13 14 15 -> 0..10: n minus the
+    // single-plane values below it (1, 2, 4, 8) minus 1
+    const int below = 1 + (n > 2) + (n > 4) + (n > 8);
+    return 32 + 11 * hi + (n - below - 1);
 }
 
 // ---- gfx950 encodings (llvm-mc -mcpu=gfx950 -show-encoding) -------------
@@ -98,40 +97,38 @@ constexpr uint32_t S_NOP0 = 0xbf800000u;
 constexpr uint32_t S_SETPC_82 = 0xbe801d52u;  // s_setpc_b64 s[82:83]
 RJ_HD inline uint32_t enc_waitcnt_lgkm(int n) { return 0xbf8cc07fu | ((uint32_t)n << 8); }
 
-// row b of the 8 x 8 GF(2) matrix of x -> c x: bit a set iff bit b of c 2^a
-RJ_HD inline void mat_rows(uint8_t c, uint8_t (&row)[8])
+// Row b of the 8 x 8 GF(2) matrix of x -> c x: bit a set iff bit b of c 2^a.
+RJ_HD inline uint8_t mat_row(uint8_t c, int b)
 {
-    uint8_t p[8];
-    uint8_t x = c;
+    uint8_t x = c, r = 0;
     for (int a = 0; a < 8; ++a) {
-        p[a] = x;
+        r |= (uint8_t)(((x >> b) & 1) << a);
         x = (uint8_t)((x << 1) ^ ((x & 0x80) ? 0x1D : 0));
     }
-    for (int b = 0; b < 8; ++b) {
-        uint8_t r = 0;
-        for (int a = 0; a < 8; ++a)
-            r |= (uint8_t)(((p[a] >> b) & 1) << a);
-        row[b] = r;
-    }
+    return r;
+}
+
+// Output plane b of the multiply-accumulate of coefficient c on slot s, bank
+// `bank` (8 bytes): acc_b ^= L[m_b & 15] ^ H[m_b >> 4], m_b = row b.
+RJ_HD inline uint64_t mac_word(uint8_t c, int s, int b, int bank)
+{
+    const uint8_t row = mat_row(c, b);
+    const int acc = ACC + 8 * s + b, lo = row & 15, hi = row >> 4;
+    if (lo && hi)
+        return enc_bitop3_96(acc, acc, table_reg(bank, 0, lo), table_reg(bank, 1, hi));
+    if (lo)
+        return enc_xor_e64(acc, acc, table_reg(bank, 0, lo));
+    if (hi)
+        return enc_xor_e64(acc, acc, table_reg(bank, 1, hi));
+    return (uint64_t)S_NOP0 << 32 | S_NOP0;  // c == 0
 }
 
 // Writes the 64 multiply-accumulate bytes of coefficient c on slot s, bank
-// `bank`, at dst (8-byte aligned): acc_b ^= L[m_b & 15] ^ H[m_b >> 4].
+// `bank`, at dst (8-byte aligned).
 RJ_HD inline void emit_mac(uint64_t* dst, uint8_t c, int s, int bank)
 {
-    uint8_t row[8];
-    mat_rows(c, row);
-    for (int b = 0; b < 8; ++b) {
-        const int acc = ACC + 8 * s + b, lo = row[b] & 15, hi = row[b] >> 4;
-        if (lo && hi)
-            dst[b] = enc_bitop3_96(acc, acc, table_reg(bank, 0, lo), table_reg(bank, 1, hi));
-        else if (lo)
-            dst[b] = enc_xor_e64(acc, acc, table_reg(bank, 0, lo));
-        else if (hi)
-            dst[b] = enc_xor_e64(acc, acc, table_reg(bank, 1, hi));
-        else  // c == 0
-            dst[b] = (uint64_t)S_NOP0 << 32 | S_NOP0;
-    }
+    for (int b = 0; b < 8; ++b)
+        dst[b] = mac_word(c, s, b, bank);
 }
 
 // Writes the 112-byte preamble of source t (of nt) at dst (8-byte aligned):

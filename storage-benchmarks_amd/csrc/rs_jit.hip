@@ -1,6 +1,6 @@
 // rs_jit.hip -- the one-matrix decode through per-block generated code
 // (rs_jit.h): dsts[b][i] = sum_p c_b[i][p] * srcs[b][p] with the e x k matrix
-// of block b baked into code that k_decode_prepare_syn wrote into executable
+// of block b baked into code that k_jit_emit wrote into executable
 // device memory (rsgpu_capi.cpp allocates it from the GPU's coarse-grained
 // pool with HSA_AMD_MEMORY_POOL_EXECUTABLE_FLAG).
 //
@@ -226,6 +226,47 @@ __global__ void k_jit_fill(uint64_t* code, long long n)
 
 }  // namespace jitk
 
+// One workgroup per (block, wave): the multiply-accumulate words one per
+// thread and iteration (coalesced), each source's preamble by one thread,
+// the chunks' ends last.  The wave's rows of the block's matrix are staged in
+// LDS first (a global load per word left the loop latency-bound), and one
+// workgroup per (block, wave, chunk) was dispatch-bound (0.49 ms for 32K
+// workgroups at C3).  Layout as rs_jit.h describes.
+__global__ __launch_bounds__(256) void k_jit_emit(int k, int e, const uint8_t* coef, const int* status,
+                                                  uint8_t* code)
+{
+    __shared__ uint8_t cw[8 * 256];  // rows 8 w .. 8 w + 7 (k <= 250)
+    const int b = blockIdx.y, w = blockIdx.x;
+    if (status[b] != 0)
+        return;
+    const int nw = (e + 7) / 8, nch = (k + 7) / 8;
+    const int nslot = min(8, e - 8 * w), per_src = nslot * 8;
+    const size_t stride = (size_t)jit::chunk_stride(8);
+    uint8_t* cbase = code + ((size_t)b * nw + w) * nch * stride;
+    for (int i = threadIdx.x; i < nslot * k; i += blockDim.x)
+        cw[i] = coef[((size_t)b * e + 8 * w) * k + i];
+    __syncthreads();
+    for (int i = threadIdx.x; i < k * per_src; i += blockDim.x) {
+        const int q = i / per_src, r = i - q * per_src, s = r >> 3, pl = r & 7;
+        const int ch = q >> 3, t = q & 7;
+        uint64_t* dst = reinterpret_cast<uint64_t*>(cbase + (size_t)ch * stride + jit::PRO_BYTES +
+                                                    (size_t)t * jit::src_bytes(nslot) + jit::PRE_BYTES);
+        dst[r] = jit::mac_word(cw[s * k + q], s, pl, t & 1);
+    }
+    for (int q = threadIdx.x; q < k; q += blockDim.x) {
+        const int ch = q >> 3, t = q & 7;
+        jit::emit_pre(reinterpret_cast<uint64_t*>(cbase + (size_t)ch * stride + jit::PRO_BYTES +
+                                                  (size_t)t * jit::src_bytes(nslot)),
+                      t, min(8, k - 8 * ch));
+    }
+    for (int ch = threadIdx.x; ch < nch; ch += blockDim.x) {
+        uint8_t* base = cbase + (size_t)ch * stride;
+        jit::emit_prologue(reinterpret_cast<uint64_t*>(base));
+        jit::emit_epilogue(
+            reinterpret_cast<uint64_t*>(base + jit::PRO_BYTES + (size_t)min(8, k - 8 * ch) * jit::src_bytes(nslot)));
+    }
+}
+
 size_t jit_code_bytes(int k, int e, long long blocks)
 {
     const int nw = (e + 7) / 8, nch = (k + 7) / 8;
@@ -236,6 +277,16 @@ hipError_t launch_jit_fill(void* code, size_t bytes, hipStream_t st)
 {
     hipLaunchKernelGGL(jitk::k_jit_fill, dim3(4096), dim3(256), 0, st, (uint64_t*)code,
                        (long long)(bytes / 8));
+    return hipGetLastError();
+}
+
+hipError_t launch_jit_emit(int k, int e, long long blocks, const uint8_t* coef, const int* status,
+                           uint8_t* code, hipStream_t st)
+{
+    if (k <= 0 || k > 250 || e <= 0 || e > 32 || blocks <= 0 || !coef || !status || !code)
+        return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_jit_emit, dim3((unsigned)((e + 7) / 8), (unsigned)blocks), dim3(256), 0, st, k, e,
+                       coef, status, code);
     return hipGetLastError();
 }
 

@@ -79,29 +79,34 @@ hipError_t launch_rs_bitsliced(int k, int e, const uint8_t* src, uint8_t* out, l
 //                        syn_addr [B][k-e][slots] of the syndrome rows
 //                        2^(r j) per surviving original j (ascending)
 // slots = tc_rows_per_pass(e); tc_table = the context's handler addresses.
-// jit_code != nullptr (with dir_addr == nullptr, one-matrix form): instead of
-// handler addresses, the straight-line code of k_rs_jit (rs_jit.h) for every
-// (block, wave, chunk) at jit_code + ((b NW + w) nch + ch) jit::chunk_stride(8).
+// jit_coef != nullptr (with dir_addr == nullptr, one-matrix form): instead of
+// handler addresses, the e x k decode rows themselves, [B][e][k] bytes, which
+// launch_jit_emit turns into k_rs_jit's code.
 hipError_t launch_decode_prepare_syn(int k, int e, long long blocks, const uint8_t* err,
                                      uint8_t* out, long long out_pitch, const uint8_t** srcs,
                                      uint8_t** dsts, const unsigned long long* tc_table,
                                      unsigned long long* tc_addr, unsigned long long* emask,
                                      int* status, unsigned long long* syn_addr,
                                      const uint8_t* src, const uint8_t* par,
-                                     unsigned long long* dir_addr, uint8_t* jit_code,
+                                     unsigned long long* dir_addr, uint8_t* jit_coef,
                                      hipStream_t st);
 
 // The one-matrix decode through generated code (rs_jit.hip).
 struct JitArgs {
     const uint8_t* const* srcs;      // [B][k]
     uint8_t* const* dsts;            // [B][rows]
-    const uint8_t* code;             // executable, written by k_decode_prepare_syn
+    const uint8_t* code;             // executable, written by k_jit_emit
     long long chunk_stride;          // jit::chunk_stride(8)
     int k, rows;                     // rows <= 32
     long long len;                   // % 32 == 0
     const int* status;               // [B]
 };
 size_t jit_code_bytes(int k, int e, long long blocks);
+// k_rs_jit's straight-line code (rs_jit.h) for every (block, wave, chunk) at
+// code + ((b NW + w) nch + ch) jit::chunk_stride(8), from the decode rows
+// coef [B][e][k] (k_decode_prepare_syn); blocks with status != 0 skipped.
+hipError_t launch_jit_emit(int k, int e, long long blocks, const uint8_t* coef, const int* status,
+                           uint8_t* code, hipStream_t st);
 hipError_t launch_jit_fill(void* code, size_t bytes, hipStream_t st);
 hipError_t launch_rs_jit(const JitArgs& a, long long blocks, hipStream_t st);
 

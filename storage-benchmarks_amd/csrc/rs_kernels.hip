@@ -875,7 +875,7 @@ __global__ __launch_bounds__(256) void k_decode_prepare_syn(int k, int e,
                                                             unsigned long long* syn_addr,
                                                             const uint8_t* src, const uint8_t* par,
                                                             unsigned long long* dir_addr,
-                                                            uint8_t* jit_code)
+                                                            uint8_t* jit_coef)
 {
     extern __shared__ __align__(16) uint8_t lds[];
     uint8_t* gexp = lds;          // 512
@@ -918,7 +918,7 @@ __global__ __launch_bounds__(256) void k_decode_prepare_syn(int k, int e,
         return (x && y) ? gexp[glog[x] + glog[y]] : (uint8_t)0;
     };
     const int tc_rows = tc_rows_per_pass(e);
-    if (dir_addr || jit_code) {
+    if (dir_addr || jit_coef) {
         // One-matrix decode through k_rs_tc: sources = the k - e surviving
         // originals (ascending) then the e parity rows, outputs = the erased
         // originals.  d_E = V_E^-1 (P ^ V_kept d_kept), V_E[p][i] = a_i^p with
@@ -1005,30 +1005,13 @@ __global__ __launch_bounds__(256) void k_decode_prepare_syn(int k, int e,
             }
             return A[i * e + (q - nl)];
         };
-        if (jit_code) {
-            // k_rs_jit's code (rs_jit.h): item (w, q) writes source q's part
-            // of wave w's chunk q / 8; items (w, ch) the chunk's ends
-            const int NW = (e + 7) / 8, nch = (k + 7) / 8;
-            const size_t stride = (size_t)jit::chunk_stride(8);
-            uint8_t* cb = jit_code + (size_t)b * NW * nch * stride;
-            for (int idx = tid; idx < NW * k; idx += nt) {
-                const int w = idx / k, q = idx - w * k;
-                const int ch = q / 8, t = q - 8 * ch, ntc = min(8, k - 8 * ch);
-                const int nslot = min(8, e - 8 * w);
-                uint64_t* dst = reinterpret_cast<uint64_t*>(cb + ((size_t)w * nch + ch) * stride +
-                                                            jit::PRO_BYTES +
-                                                            (size_t)t * jit::src_bytes(nslot));
-                jit::emit_pre(dst, t, ntc);
-                for (int s = 0; s < nslot; ++s)
-                    jit::emit_mac(dst + jit::PRE_BYTES / 8 + 8 * s, dcoef(q, 8 * w + s), s, t & 1);
-            }
-            for (int idx = tid; idx < NW * nch; idx += nt) {
-                const int w = idx / nch, ch = idx - w * nch, ntc = min(8, k - 8 * ch);
-                const int nslot = min(8, e - 8 * w);
-                uint8_t* base = cb + ((size_t)w * nch + ch) * stride;
-                jit::emit_prologue(reinterpret_cast<uint64_t*>(base));
-                jit::emit_epilogue(reinterpret_cast<uint64_t*>(
-                    base + jit::PRO_BYTES + (size_t)ntc * jit::src_bytes(nslot)));
+        if (jit_coef) {
+            // k_rs_jit's decode rows [e][k] for k_jit_emit (coalesced here,
+            // the code is written by one workgroup per (wave, chunk) there)
+            uint8_t* cb = jit_coef + (size_t)b * e * k;
+            for (int idx = tid; idx < e * k; idx += nt) {
+                const int i = idx / k, q = idx - i * k;
+                cb[idx] = dcoef(q, i);
             }
             return;
         }
@@ -1150,11 +1133,11 @@ hipError_t launch_decode_prepare_syn(int k, int e, long long blocks, const uint8
                                      unsigned long long* tc_addr, unsigned long long* emask,
                                      int* status, unsigned long long* syn_addr,
                                      const uint8_t* src, const uint8_t* par,
-                                     unsigned long long* dir_addr, uint8_t* jit_code,
+                                     unsigned long long* dir_addr, uint8_t* jit_coef,
                                      hipStream_t st)
 {
     if (k <= 0 || k > 250 || e <= 0 || e > 32 ||
-        (!jit_code && (!tc_table || (!dir_addr && (!tc_addr || !syn_addr)))))
+        (!jit_coef && (!tc_table || (!dir_addr && (!tc_addr || !syn_addr)))))
         return hipErrorInvalidValue;
     static bool attr_set = false;
     if (!attr_set) {
@@ -1164,7 +1147,7 @@ hipError_t launch_decode_prepare_syn(int k, int e, long long blocks, const uint8
     }
     hipLaunchKernelGGL(k_decode_prepare_syn, dim3((unsigned)blocks), dim3(256),
                        decode_prepare_syn_lds_bytes(e), st, k, e, err, out, out_pitch, srcs, dsts,
-                       tc_table, tc_addr, emask, status, syn_addr, src, par, dir_addr, jit_code);
+                       tc_table, tc_addr, emask, status, syn_addr, src, par, dir_addr, jit_coef);
     return hipGetLastError();
 }
 

@@ -749,6 +749,10 @@ int rsgpu_ec_encode_data_update(rsgpu_ctx* ctx, int len, int k, int rows, int ve
 
 // ---- device, batched -----------------------------------------------------------
 
+// Most kernels put the block index in grid.y (or z), whose limit is 65535:
+// the block-batched entry points run larger batches as consecutive slices.
+constexpr size_t kMaxGridBlocks = 65535;
+
 static int check_geom(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch, size_t blocks)
 {
     if (!ctx)
@@ -767,6 +771,15 @@ int rsgpu_encode_blocks(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch, 
         return rc;
     if (e == 0 || len == 0)
         return RSGPU_OK;
+    if (blocks > kMaxGridBlocks) {
+        for (size_t b0 = 0; b0 < blocks; b0 += kMaxGridBlocks) {
+            rc = rsgpu_encode_blocks(ctx, k, e, len, pitch, std::min(kMaxGridBlocks, blocks - b0),
+                                     d_src + b0 * k * pitch, d_parity + b0 * e * pitch, coef);
+            if (rc)
+                return rc;
+        }
+        return RSGPU_OK;
+    }
     const bool aligned = ((uintptr_t)d_src % 16 == 0) && ((uintptr_t)d_parity % 16 == 0) &&
                          (pitch % 16 == 0);
     // Fast paths: the gf_gen_rs_matrix code with compile-time coefficients,
@@ -828,6 +841,9 @@ enum class Plan {
     general_dot  // k_decode_prepare + k_dot_generic (unaligned / odd lengths)
 };
 
+// column tiles (2 KB) per block from which AUTO decodes through generated code
+constexpr size_t kJitMinTiles = 128;
+
 bool rows_aligned(size_t len, size_t pitch, const void* a, const void* b, const void* c)
 {
     return len % 32 == 0 && pitch % 16 == 0 && (uintptr_t)a % 16 == 0 && (uintptr_t)b % 16 == 0 &&
@@ -846,7 +862,13 @@ Plan decode_plan(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch, const v
         return Plan::fused;
     if (want == RSGPU_DECODE_ONE_MATRIX || jit_probe(ctx) != 1)
         return Plan::one_matrix;
-    return Plan::generated;  // AUTO / GENERATED
+    // AUTO: generated code only when a block has enough column tiles to
+    // amortise its ~160 KB of code (every tile's workgroup fetches all of
+    // it): C3 / C5 (489 tiles) 25.2 / 15.0 ms vs 27 / 17.7 threaded; C4
+    // (16 tiles) 16.6 + 4.7 prepare vs 14.9 + 0.4 (profiles/r02_ab)
+    if (want == RSGPU_DECODE_AUTO && (len + 2047) / 2048 < kJitMinTiles)
+        return Plan::one_matrix;
+    return Plan::generated;
 }
 
 // Workspace: [emask B x 16 B | survivor ptrs B x k | output ptrs B x e |
@@ -970,6 +992,9 @@ int rsgpu_decode_prepare(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch,
         return RSGPU_OK;
     if (e > k || !d_err || !d_workspace || !d_status)
         return fail(ctx, RSGPU_ERR_ARG, "rsgpu_decode_prepare: bad arguments");
+    if (blocks > kMaxGridBlocks)
+        return fail(ctx, RSGPU_ERR_ARG, "rsgpu_decode_prepare: at most 65535 blocks per call "
+                                        "(rsgpu_decode_blocks slices larger batches)");
     const Plan plan = decode_plan(ctx, k, e, len, pitch, d_src, d_parity, d_out);
     if (plan == Plan::one_matrix || plan == Plan::fused || plan == Plan::generated) {
         const WsLayout w = ws_layout(k, e, blocks);
@@ -980,15 +1005,23 @@ int rsgpu_decode_prepare(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch,
             if (rc)
                 return rc;
         }
-        KTimer kt(ctx, "k_decode_prepare_syn", blocks);
-        RS_HIP(ctx, launch_decode_prepare_syn(
-                        k, e, (long long)blocks, d_err, d_out, (long long)pitch,
-                        (const uint8_t**)(ws + w.surv), (uint8_t**)(ws + w.outp), ctx->d_tc_table,
-                        plan == Plan::fused ? (unsigned long long*)(ws + w.tab) : nullptr,
-                        (unsigned long long*)ws, d_status,
-                        plan == Plan::fused ? (unsigned long long*)(ws + w.tab2) : nullptr, d_src,
-                        d_parity, one ? (unsigned long long*)(ws + w.tab) : nullptr,
-                        gen ? (uint8_t*)ctx->d_jit : nullptr, ctx->stream));
+        {
+            KTimer kt(ctx, "k_decode_prepare_syn", blocks);
+            RS_HIP(ctx, launch_decode_prepare_syn(
+                            k, e, (long long)blocks, d_err, d_out, (long long)pitch,
+                            (const uint8_t**)(ws + w.surv), (uint8_t**)(ws + w.outp), ctx->d_tc_table,
+                            plan == Plan::fused ? (unsigned long long*)(ws + w.tab) : nullptr,
+                            (unsigned long long*)ws, d_status,
+                            plan == Plan::fused ? (unsigned long long*)(ws + w.tab2) : nullptr, d_src,
+                            d_parity, one ? (unsigned long long*)(ws + w.tab) : nullptr,
+                            gen ? (uint8_t*)(ws + w.tab) : nullptr, ctx->stream));
+        }
+        if (gen) {
+            // the decode rows [B][e][k] sit in the coefficient region
+            KTimer ke(ctx, "k_jit_emit", blocks);
+            RS_HIP(ctx, launch_jit_emit(k, e, (long long)blocks, (const uint8_t*)(ws + w.tab), d_status,
+                                        (uint8_t*)ctx->d_jit, ctx->stream));
+        }
         return RSGPU_OK;
     }
     return general_prepare(ctx, plan, k, k + e, e, true, pitch, blocks, nullptr, d_src, d_parity,
@@ -1006,6 +1039,9 @@ int rsgpu_decode_apply(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch, s
         return RSGPU_OK;
     if (e > k || !d_workspace || !d_status)
         return fail(ctx, RSGPU_ERR_ARG, "rsgpu_decode_apply: bad arguments");
+    if (blocks > kMaxGridBlocks)
+        return fail(ctx, RSGPU_ERR_ARG, "rsgpu_decode_apply: at most 65535 blocks per call "
+                                        "(rsgpu_decode_blocks slices larger batches)");
     const Plan plan = decode_plan(ctx, k, e, len, pitch, d_src, d_parity, d_out);
     const WsLayout w = ws_layout(k, e, blocks);
     char* ws = (char*)d_workspace;
@@ -1052,6 +1088,19 @@ int rsgpu_decode_blocks(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch, 
                         const unsigned char* d_err, unsigned char* d_out, void* d_workspace,
                         int* d_status)
 {
+    if (blocks > kMaxGridBlocks) {
+        // slices in stream order, each through the start of the workspace
+        // (a slice's layout is no larger than the whole batch's)
+        for (size_t b0 = 0; b0 < blocks; b0 += kMaxGridBlocks) {
+            const int rc = rsgpu_decode_blocks(
+                ctx, k, e, len, pitch, std::min(kMaxGridBlocks, blocks - b0), d_src + b0 * k * pitch,
+                d_parity + b0 * e * pitch, d_err ? d_err + b0 * e : nullptr, d_out + b0 * e * pitch,
+                d_workspace, d_status ? d_status + b0 : nullptr);
+            if (rc)
+                return rc;
+        }
+        return RSGPU_OK;
+    }
     int rc = rsgpu_decode_prepare(ctx, k, e, len, pitch, blocks, d_src, d_parity, d_err, d_out,
                                   d_workspace, d_status);
     if (rc)
@@ -1081,6 +1130,17 @@ int rsgpu_decode_general(rsgpu_ctx* ctx, int k, int m, size_t len, size_t pitch,
         return RSGPU_OK;
     if (!d_err || !d_workspace || !d_status || !d_out)
         return fail(ctx, RSGPU_ERR_ARG, "rsgpu_decode_general: bad arguments");
+    if (blocks > kMaxGridBlocks) {
+        for (size_t b0 = 0; b0 < blocks; b0 += kMaxGridBlocks) {
+            rc = rsgpu_decode_general(ctx, k, m, len, pitch, std::min(kMaxGridBlocks, blocks - b0),
+                                      encode_matrix, d_src + b0 * k * pitch, d_parity + b0 * (m - k) * pitch,
+                                      d_err + b0 * nerrs, nerrs, d_out + b0 * nerrs * pitch, d_workspace,
+                                      d_status + b0);
+            if (rc)
+                return rc;
+        }
+        return RSGPU_OK;
+    }
     const bool tcp = rows_aligned(len, pitch, d_src, d_parity, d_out) && tc_ready(ctx);
     const Plan plan = tcp ? Plan::general_tc : Plan::general_dot;
     const uint8_t* d_enc = nullptr;
@@ -1117,6 +1177,16 @@ int rsgpu_verify_blocks(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch, 
         return rc;
     if (e == 0 || len == 0)
         return RSGPU_OK;
+    if (blocks > kMaxGridBlocks) {
+        for (size_t b0 = 0; b0 < blocks; b0 += kMaxGridBlocks) {
+            rc = rsgpu_verify_blocks(ctx, k, e, len, pitch, std::min(kMaxGridBlocks, blocks - b0),
+                                     d_src + b0 * k * pitch, d_out + b0 * e * pitch, d_err + b0 * e,
+                                     d_mismatch + b0);
+            if (rc)
+                return rc;
+        }
+        return RSGPU_OK;
+    }
     RS_HIP(ctx, launch_compare_rows(d_src, (long long)pitch, k, d_out, (long long)pitch, e, d_err,
                                     (long long)len, (long long)blocks, d_mismatch, ctx->stream));
     return RSGPU_OK;

@@ -388,3 +388,38 @@ def test_bench_c4_streams_ragged_batches():
     st = line["streamed"]
     assert st["batches"] == 3 and st["blocks_total"] == 2500 and st["mismatch_bytes"] == 0
     assert "blocks=2500" in line["config"]["workload"]
+
+
+@pytest.mark.parametrize("kernel", ["auto", "generated", "one_matrix"])
+def test_batch_beyond_grid_limit(ctx, orc, kernel):
+    """70000 blocks in one call (more than the 65535 a grid dimension holds):
+    encode, decode (erased rows poisoned) and verify run as consecutive
+    slices; every block is verified on the device and sampled blocks on
+    either side of the slice boundary are compared with the oracle."""
+    k, e, L, B = 6, 3, 64, 70000
+    ctx.set_decode_kernel(kernel)
+    try:
+        enc = rsgpu.GpuEncoder(k, L, e, blocks=B, seed=11, ctx=ctx)
+        enc.encode_all()
+        dec = rsgpu.GpuDecoder(k, L, e, blocks=B, seed=11, ctx=ctx)
+        src = enc.src.view(B, k, enc.pitch)
+        keep = src[:, :, :L].clone()
+        # poison every erased original of every block (vectorised)
+        errs = torch.from_numpy(dec.err_host.astype(np.int64)).to(src.device)
+        src.scatter_(1, errs[:, :, None].expand(B, e, enc.pitch), 0xA5)
+        dec.decode_all(enc)
+        torch.cuda.synchronize()
+        src[:, :, :L] = keep
+        assert dec.is_complete() and dec.verify_data(enc)
+        out = dec.out.view(B, e, dec.pitch)
+        for b in (0, 1, 65534, 65535, 65536, B - 1):
+            data = [keep[b, j].cpu().numpy() for j in range(k)]
+            par = enc.parity_rows(b)
+            ref = orc.encode_block(data, e)
+            assert all((par[i] == ref[i]).all() for i in range(e)), b
+            rc, rec = orc.decode_block(data, list(par), dec.err_host[b])
+            assert rc == 0
+            got = out[b, :, :L].cpu().numpy()
+            assert all((got[i] == rec[i]).all() for i in range(e)), b
+    finally:
+        ctx.set_decode_kernel("auto")

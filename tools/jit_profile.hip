@@ -57,6 +57,8 @@ int main(int argc, char** argv)
     const int B = argc > 1 ? atoi(argv[1]) : 512;
     const int k = argc > 2 ? atoi(argv[2]) : 64;
     const int e = argc > 3 ? atoi(argv[3]) : 32;
+    // extra dynamic LDS per workgroup: caps workgroups per CU (occupancy A/B)
+    const int extra_lds = argc > 4 ? atoi(argv[4]) : 0;
     const long long L = 1000000, pitch = 1000192;
     uint8_t* rows;
     if (hipMalloc(&rows, (size_t)B * (k + e) * pitch) != hipSuccess) {
@@ -145,7 +147,11 @@ int main(int argc, char** argv)
         (void)hipEventCreate(&e0);
         (void)hipEventCreate(&e1);
         (void)hipEventRecord(e0);
-        (void)launch_rs_jit(a, B, 0);
+        if (extra_lds && e > 24)
+            hipLaunchKernelGGL(jitk::k_rs_jit<4>, dim3((unsigned)((L + 2047) / 2048), (unsigned)B), dim3(256),
+                               extra_lds, 0, a);
+        else
+            (void)launch_rs_jit(a, B, 0);
         (void)hipEventRecord(e1);
         if (hipDeviceSynchronize() != hipSuccess) {
             printf("kernel failed\n");
