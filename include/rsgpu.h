@@ -128,14 +128,19 @@ size_t rsgpu_decode_workspace_bytes(int k, int e, size_t blocks);
 
 /* Decode kernel of rsgpu_decode_blocks (per context; every choice recovers
  * the same bytes):
- *   AUTO        the measured-fastest choice per code (the default)
+ *   AUTO        GENERATED when a block has >= 128 column tiles of 2 KB
+ *               (len > 254 KiB), else ONE_MATRIX (the default)
  *   ONE_MATRIX  closed-form e x k decode rows V_E^-1 [V_kept | I] (e <= 32),
  *               one threaded-code pass over the k - e survivors + e parity
  *   FUSED       syndromes and the e x e solve per column tile in one kernel
  *               (e <= 32, k <= 128)
  *   GENERAL     the reference's k x k survivor-matrix inversion on the
  *               device (isa.cpp:177-204), then the decode rows; any e
- * A choice that does not apply to a geometry falls back to GENERAL. */
+ *   GENERATED   the ONE_MATRIX rows baked into per-block straight-line code
+ *               (written to executable device memory by the prepare step),
+ *               one call per chunk of 8 sources (e <= 32)
+ * A choice that does not apply to a geometry falls back to GENERAL (e > 32,
+ * unaligned rows) or ONE_MATRIX. */
 #define RSGPU_DECODE_AUTO 0
 #define RSGPU_DECODE_ONE_MATRIX 1
 #define RSGPU_DECODE_FUSED 2
@@ -152,7 +157,9 @@ int rsgpu_set_decode_kernel(rsgpu_ctx *ctx, int kernel);
  * -1 for a singular matrix ("BAD MATRIX", isa.cpp:185-190); -2 for a
  * malformed erasure list (not strictly ascending, or an index >= k).  A
  * block with a non-zero status is skipped; its output is unspecified.
- * d_workspace holds rsgpu_decode_workspace_bytes() bytes. */
+ * d_workspace holds rsgpu_decode_workspace_bytes() bytes.  Batches of more
+ * than 65535 blocks run as consecutive slices (as do rsgpu_encode_blocks,
+ * rsgpu_decode_general and rsgpu_verify_blocks). */
 int rsgpu_decode_blocks(rsgpu_ctx *ctx, int k, int e, size_t len, size_t pitch, size_t blocks,
                         const unsigned char *d_src, const unsigned char *d_parity,
                         const unsigned char *d_err, unsigned char *d_out, void *d_workspace,
@@ -164,7 +171,8 @@ int rsgpu_decode_blocks(rsgpu_ctx *ctx, int k, int e, size_t len, size_t pitch, 
  * (isa.cpp:208-209) for blocks whose status is 0.  decode_blocks ==
  * prepare followed by apply on the same stream.  apply may fan work out to an
  * internal second stream; it always joins back, so everything it wrote is
- * ordered before later work on the context stream. */
+ * ordered before later work on the context stream.  At most 65535 blocks
+ * per call (RSGPU_ERR_ARG beyond). */
 int rsgpu_decode_prepare(rsgpu_ctx *ctx, int k, int e, size_t len, size_t pitch, size_t blocks,
                          const unsigned char *d_src, const unsigned char *d_parity,
                          const unsigned char *d_err, unsigned char *d_out, void *d_workspace,

@@ -17,6 +17,7 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/mman.h>
 #include <time.h>
 
 #include "erasure_code.h"
@@ -151,6 +152,24 @@ static int decode_block_with(data_kernel_t kern, int k, int e, int len,
 /* 165-177).                                                                 */
 /* ------------------------------------------------------------------------ */
 
+/* Row buffers of the CPU baseline: each its own anonymous mapping, so every
+ * row starts on a page boundary whatever the allocator did before.  (With
+ * glibc's aligned_alloc the rows came from mmap on a fresh process but from
+ * the heap after earlier frees had raised the mmap threshold; in that state
+ * the port's decode ran at 1.5-2x its encode time on the GPU box's host,
+ * tools/cpu_asym.py, profiles/r02_cpu_asym.json.) */
+static unsigned char *row_alloc(size_t len)
+{
+    void *p = mmap(NULL, len ? len : 1, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+    return p == MAP_FAILED ? NULL : (unsigned char *)p;
+}
+
+static void row_free(unsigned char *p, size_t len)
+{
+    if (p)
+        munmap(p, len ? len : 1);
+}
+
 static inline uint64_t mix64(uint64_t z)
 {
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
@@ -181,10 +200,10 @@ static void *worker(void *arg)
     unsigned char **par = malloc(sizeof(void *) * (size_t)(e ? e : 1));
     unsigned char **out = malloc(sizeof(void *) * (size_t)(e ? e : 1));
     for (int i = 0; i < k; ++i)
-        data[i] = aligned_alloc(64, ((size_t)len + 63) / 64 * 64);
+        data[i] = row_alloc((size_t)len);
     for (int i = 0; i < e; ++i) {
-        par[i] = aligned_alloc(64, ((size_t)len + 63) / 64 * 64);
-        out[i] = aligned_alloc(64, ((size_t)len + 63) / 64 * 64);
+        par[i] = row_alloc((size_t)len);
+        out[i] = row_alloc((size_t)len);
     }
     /* outputs pre-touched outside the timed region, so the timed kernels do
      * not pay first-touch page faults (the reference's posix_memalign'd
@@ -228,10 +247,10 @@ static void *worker(void *arg)
                     j->failures++;
     }
     for (int i = 0; i < k; ++i)
-        free(data[i]);
+        row_free(data[i], (size_t)len);
     for (int i = 0; i < e; ++i) {
-        free(par[i]);
-        free(out[i]);
+        row_free(par[i], (size_t)len);
+        row_free(out[i], (size_t)len);
     }
     free(data); free(par); free(out);
     (void)m;
@@ -285,4 +304,111 @@ double ref_cpu_bench_kernel(int k, int e, int len, int threads, int blocks_per_t
     free(jobs);
     free(th);
     return wall;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Diagnostic for the CPU baseline's decode/encode asymmetry (bench.py       */
+/* reports the port's decode at ~2x its encode on the GPU box): one thread,  */
+/* the worker's allocation and generation pattern, per rep:                  */
+/*   t[0] encode_block_with (as timed by the baseline)                       */
+/*   t[1] decode_block_with (as timed by the baseline)                       */
+/*   t[2] the decode's data kernel alone, same survivors and outputs, again  */
+/*   t[3] the encode's data kernel alone, again                              */
+/*   t[4] the decode's data kernel into fresh (pre-touched) outputs          */
+/* ------------------------------------------------------------------------ */
+void ref_cpu_asym(int k, int e, int len, int reps, double *t)
+{
+    unsigned char **data = malloc(sizeof(void *) * (size_t)k);
+    unsigned char **par = malloc(sizeof(void *) * (size_t)e);
+    unsigned char **out = malloc(sizeof(void *) * (size_t)e);
+    unsigned char **out2 = malloc(sizeof(void *) * (size_t)e);
+    unsigned char **surv = malloc(sizeof(void *) * (size_t)k);
+    for (int i = 0; i < k; ++i)
+        data[i] = row_alloc((size_t)len);
+    for (int i = 0; i < e; ++i) {
+        par[i] = row_alloc((size_t)len);
+        out[i] = row_alloc((size_t)len);
+        out2[i] = row_alloc((size_t)len);
+        memset(par[i], 0, (size_t)len);
+        memset(out[i], 0, (size_t)len);
+        memset(out2[i], 0, (size_t)len);
+    }
+    int m = k + e;
+    unsigned char *a = malloc((size_t)m * k), *g = malloc((size_t)32 * k * e);
+    unsigned char err[256], in_err[256];
+    gf_gen_rs_matrix(a, m, k);
+    ec_init_tables(k, e, &a[k * k], g);
+    for (int q = 0; q < 5; ++q)
+        t[q] = 0;
+    for (int r = 0; r < reps; ++r) {
+        for (int i = 0; i < k; ++i)
+            for (int p = 0; p < len; p += 8) {
+                uint64_t v = mix64((uint64_t)r * 0x9E3779B97F4A7C15ull + (uint64_t)i * 0xD1B54A32D192ED03ull + (uint64_t)p / 8);
+                for (int q = 0; q < 8 && p + q < len; ++q)
+                    data[i][p + q] = (unsigned char)(v >> (8 * q));
+            }
+        memset(in_err, 0, sizeof(in_err));
+        for (int have = 0, ctr = 0; have < e; ++ctr) {
+            int s = (int)(mix64((uint64_t)r * 0x2545F4914F6CDD1Dull ^ (uint64_t)ctr) % (uint64_t)k);
+            if (!in_err[s]) {
+                in_err[s] = 1;
+                ++have;
+            }
+        }
+        for (int i = 0, n = 0; i < k; ++i)
+            if (in_err[i])
+                err[n++] = (unsigned char)i;
+        for (int i = 0, q = 0; i < k; ++i)
+            if (!in_err[i])
+                surv[q++] = data[i];
+        for (int i = 0; i < e; ++i)
+            surv[k - e + i] = par[i];
+        double t0 = now_s();
+        encode_block_with(port_ec_encode_data_avx2, k, e, len, data, par);
+        double t1 = now_s();
+        decode_block_with(port_ec_encode_data_avx2, k, e, len, err, data, par, out);
+        double t2 = now_s();
+        port_ec_encode_data_avx2(len, k, e, g, surv, out);
+        double t3 = now_s();
+        port_ec_encode_data_avx2(len, k, e, g, data, par);
+        double t4 = now_s();
+        port_ec_encode_data_avx2(len, k, e, g, surv, out2);
+        double t5 = now_s();
+        t[0] += t1 - t0;
+        t[1] += t2 - t1;
+        t[2] += t3 - t2;
+        t[3] += t4 - t3;
+        t[4] += t5 - t4;
+    }
+    for (int q = 0; q < 5; ++q)
+        t[q] /= reps;
+    for (int i = 0; i < k; ++i)
+        row_free(data[i], (size_t)len);
+    for (int i = 0; i < e; ++i) {
+        row_free(par[i], (size_t)len);
+        row_free(out[i], (size_t)len);
+        row_free(out2[i], (size_t)len);
+    }
+    free(data); free(par); free(out); free(out2); free(surv); free(a); free(g);
+}
+
+typedef struct {
+    int k, e, len, reps;
+    double *t;
+} asym_job_t;
+
+static void *asym_worker(void *arg)
+{
+    asym_job_t *j = (asym_job_t *)arg;
+    ref_cpu_asym(j->k, j->e, j->len, j->reps, j->t);
+    return NULL;
+}
+
+/* ref_cpu_asym on a fresh pthread, as the baseline's workers run */
+void ref_cpu_asym_thread(int k, int e, int len, int reps, double *t)
+{
+    asym_job_t j = {k, e, len, reps, t};
+    pthread_t th;
+    pthread_create(&th, NULL, asym_worker, &j);
+    pthread_join(th, NULL);
 }
