@@ -14,8 +14,8 @@
 // mode.
 //
 // The instruction cache is not invalidated between kernel launches, and the
-// code of a block is rewritten by every prepare, so each wave executes
-// s_icache_inv before its first call (measured free: tools/ubench_jit.hip).
+// code of a block is rewritten by every prepare, so wave 0 of every workgroup
+// executes s_icache_inv before the workgroup's first call.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -119,7 +119,15 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_num_vgpr(64))) void 
     const long long off = tile * 2048 + lane * 32;
     const long long loff = off + 32 <= a.len ? off : 0;  // out-of-range lanes re-read the row head
 
-    asm volatile("s_icache_inv\n s_nop 15\n s_nop 15" ::: "memory");
+    // The instruction cache is shared by the waves of a CU pair and keeps
+    // lines across launches: wave 0 invalidates it before any wave of this
+    // workgroup calls code (the calls follow the first chunk barrier).  Every
+    // wave invalidating measured 1.3 % slower (it wipes the other workgroups'
+    // lines too; profiles/r02_ab/jit_icache_inv.log).
+#ifndef RSGPU_JIT_NO_INV  // timing-only builds: code unchanged between launches
+    if (wave == 0)
+        asm volatile("s_icache_inv\n s_nop 15\n s_nop 15" ::: "memory");
+#endif
 
     // chunk ch's sources this wave moves: t = wave, wave + NW, ... (two row
     // pointers per scalar wait)
