@@ -46,7 +46,11 @@ constexpr int ACC = 64;          // accumulator base register
 constexpr int LDS_SRC = 2048;    // LDS bytes per source: [2 halves][64 lanes] x 16 B
 constexpr int LDS_HALF = 1024;
 constexpr int PRO_BYTES = 16;
+#ifndef RSGPU_JIT_NCOMP
 constexpr int PRE_BYTES = 112;   // per source before the multiply-accumulates
+#else  // timing-only builds (tools/jit_profile): the first RSGPU_JIT_NCOMP composites only
+constexpr int PRE_BYTES = (20 + 4 * RSGPU_JIT_NCOMP + 7) / 8 * 8;
+#endif
 constexpr int EPI_BYTES = 8;
 
 RJ_HD constexpr int src_bytes(int nslot) { return PRE_BYTES + 64 * nslot; }
@@ -154,11 +158,16 @@ RJ_HD inline void emit_pre(uint64_t* dst, int t, int nt)
     for (int hi = 0; hi < 2; ++hi)
         for (int n = 1; n < 16; ++n) {
             const int low = n & -n;
+#ifdef RSGPU_JIT_NCOMP
+            if (i >= 5 + RSGPU_JIT_NCOMP)
+                break;
+#endif
             if (n != low)
                 w[i++] = enc_xor_e32(table_reg(bank, hi, n), table_reg(bank, hi, n ^ low),
                                      table_reg(bank, hi, low));
         }
-    w[i++] = S_NOP0;  // i == 28: 112 bytes
+    while (i < PRE_BYTES / 4)
+        w[i++] = S_NOP0;  // 112 bytes
 }
 
 // prologue (source 0's planes into bank A) at the chunk start
