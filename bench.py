@@ -63,9 +63,14 @@ def parse(argv=None):
     p.add_argument("--blocks", type=int, default=None,
                    help="blocks per GPU (c4: blocks in total) override")
     p.add_argument("--batch", type=int, default=C4_BATCH, help="c4: resident blocks per batch")
+    p.add_argument("--symbols", type=int, default=None, help="override the config's symbols (k)")
+    p.add_argument("--symbol-size", type=int, default=None, help="override the config's symbol_size (L)")
+    p.add_argument("--loss-rate", type=float, default=None, help="override the config's loss_rate")
     p.add_argument("--seed", type=int, default=1)
     p.add_argument("--decode-kernel", default="auto",
                    choices=["auto", "generated", "one_matrix", "fused", "general"])
+    p.add_argument("--encode-kernel", default="auto",
+                   choices=["auto", "compiled", "generated", "threaded"])
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-threads", type=int, default=None)
     p.add_argument("--no-ref-base", action="store_true",
@@ -408,6 +413,7 @@ def alg_bytes(k, e, L):
     return {"k_rs_bs(encode)": blk_op, "k_rs_encode_lh": blk_op, "k_dot_generic": blk_op,
             "k_dot_generic(decode)": blk_op, "k_rs_decode_fused": blk_op,
             "k_rs_tc(encode)": blk_op, "k_rs_tc(decode)": blk_op, "k_rs_jit(decode)": blk_op,
+            "k_rs_jit(encode)": blk_op,
             "k_decode_prepare": 0.0, "k_decode_prepare_syn": 0.0}
 
 
@@ -522,12 +528,17 @@ def main(argv=None):
     import rsgpu
 
     k, L, loss, B = CONFIGS[args.config]
+    custom = args.symbols is not None or args.symbol_size is not None or args.loss_rate is not None
+    k = args.symbols if args.symbols is not None else k
+    L = args.symbol_size if args.symbol_size is not None else L
+    loss = args.loss_rate if args.loss_rate is not None else loss
     if args.blocks:
         B = args.blocks
     e = int(math.ceil(k * loss))
     ctx = rsgpu.Context(dev.index)
     ctx.set_torch_stream()
     ctx.set_decode_kernel(args.decode_kernel)
+    ctx.set_encode_kernel(args.encode_kernel)
     alg = alg_bytes(k, e, L)
     rank_info = None
 
@@ -608,7 +619,7 @@ def main(argv=None):
         out_bytes_step = 2.0 * e * L * B            # parity + recovered, per rank
         value = job_goodput(out_bytes_step, steps, world, elapsed)
         ms_step = elapsed / steps * 1e3
-        workload = (f"isa_throughput {args.config}: symbols={k} symbol_size={L} loss_rate={loss} "
+        workload = (f"isa_throughput {args.config}{' (custom geometry)' if custom else ''}: symbols={k} symbol_size={L} loss_rate={loss} "
                     f"erased={e} blocks_per_gpu={B}")
         extra = {}
 
@@ -624,7 +635,8 @@ def main(argv=None):
     # same command (counters cannot be read inside this timed run); only
     # valid for the C3 workload they were measured on
     traffic, traffic_src = None, None
-    if args.traffic and os.path.exists(args.traffic) and args.config == "c3" and not args.blocks:
+    if (args.traffic and os.path.exists(args.traffic) and args.config == "c3" and not args.blocks
+            and not custom):
         traffic = json.load(open(args.traffic)).get(dom)
         traffic_src = os.path.relpath(args.traffic, ROOT) if traffic is not None else None
     op_bytes = float((k + e) * L) * (out_bytes_step / (2.0 * e * L))
@@ -639,7 +651,7 @@ def main(argv=None):
         "config": {"workload": workload, "symbols": k, "symbol_size": L, "loss_rate": loss,
                    "erased": e, "blocks_per_gpu": out_bytes_step / (2.0 * e * L),
                    "parallelism": f"blocks sharded x{world}, no collective",
-                   "decode_kernel": args.decode_kernel},
+                   "decode_kernel": args.decode_kernel, "encode_kernel": args.encode_kernel},
         "hbm_roofline_frac_step": round(step_frac, 4),
         "kernels": kernels,
         "verified": ok,

@@ -122,6 +122,24 @@ int rsgpu_encode_blocks(rsgpu_ctx *ctx, int k, int e, size_t len, size_t pitch, 
                         const unsigned char *d_src, unsigned char *d_parity,
                         const unsigned char *coef);
 
+/* Encode kernel of rsgpu_encode_blocks / rsgpu_ec_encode_data (per context;
+ * every choice writes the same bytes):
+ *   AUTO       COMPILED for the codes built in (gf_gen_rs_matrix (k, e) in
+ *              {(16,4) (16,8) (64,32) (64,16) (100,20) (5,4) (20,7)}, no
+ *              `coef`), otherwise GENERATED (aligned rows, len % 32 == 0),
+ *              otherwise the v_perm kernel
+ *   COMPILED   k_rs_bs: the matrix compiled into the kernel (codes above)
+ *   GENERATED  k_rs_jit with code built on the host for the matrix, once,
+ *              shared by every block: per source only the composites its
+ *              coefficients need (greedy cover); rows in passes of 32
+ *   THREADED   k_rs_tc: 256 generated handlers, one dispatch per coefficient
+ * A choice that does not apply falls back in that order. */
+#define RSGPU_ENCODE_AUTO 0
+#define RSGPU_ENCODE_COMPILED 1
+#define RSGPU_ENCODE_GENERATED 2
+#define RSGPU_ENCODE_THREADED 3
+int rsgpu_set_encode_kernel(rsgpu_ctx *ctx, int kernel);
+
 /* Device workspace needed by rsgpu_decode_blocks for this geometry (any
  * decode kernel choice). */
 size_t rsgpu_decode_workspace_bytes(int k, int e, size_t blocks);

@@ -1,0 +1,55 @@
+// jit_prog.h -- host-built generated code for a coefficient matrix shared by
+// every block (the runtime-coefficient encode: caller `coef`, Cauchy,
+// ec_encode_data's gftbls, codes without a compile-time kernel).
+//
+// The code runs in k_rs_jit (rs_jit.hip) exactly like the per-block decode
+// code, with the register contract of rs_jit.h, but each (wave, source)
+// preamble builds only the composites its 64 masks need: a greedy cover
+// (the algorithm of gen_enc_progs.py, which serves the compile-time encode)
+// picks XORs of 2 or 3 available values until every mask is the XOR of at
+// most two values, so the multiply-accumulate stays one instruction per
+// output plane.  13.4 composites per source for random coefficients against
+// the 22 of the full four-Russians tables; when a cover would need more than
+// 22, the full tables serve.  Everything here runs on the host: the matrix
+// is known there, and the code is built once per matrix and cached.
+#pragma once
+#include <stddef.h>
+#include <stdint.h>
+
+#include <vector>
+
+namespace rsgpu {
+namespace jit {
+
+constexpr int kMaxComposites = 22;  // v32..v53
+constexpr uint8_t kNone = 255;
+
+// One (wave, source) program: value ids 0..7 are the source's planes
+// (bit i of a mask = plane i), 8 + i the composite ops[i] = XOR of its 2 or 3
+// operand values; accumulator plane b of slot s gets outs[8 s + b] (0, 1 or
+// 2 values) XORed in.
+struct SrcProg {
+    int nops = 0;
+    uint8_t ops[kMaxComposites][3];
+    uint8_t outs[64][2];
+};
+
+// Cover of the masks of coefficients coef[0..nslot-1] (slot s = output row
+// 8 w + s of the wave).
+void plan_source(const uint8_t* coef, int nslot, SrcProg& p);
+
+// Largest chunk (8 sources, 8 slots, kMaxComposites 3-input composites),
+// rounded to 64-byte lines: the stride between chunks of host-built code.
+int host_chunk_stride();
+
+// Code of one chunk (nt <= 8 sources with programs progs[0..nt-1], nslot <=
+// 8 slots) at dst; returns its size in bytes (<= host_chunk_stride()).
+size_t emit_chunk(uint8_t* dst, int nt, int nslot, const SrcProg* progs);
+
+// The whole program of an e x k matrix c (row-major) in passes of <= 32
+// rows: pass p, wave w, chunk ch at ((p NW_MAX + w) nch + ch) stride, with
+// NW_MAX = 4 wave slots reserved per pass.  Returns the bytes.
+std::vector<uint8_t> build_matrix_code(const uint8_t* c, int k, int e, int* chunk_stride);
+
+}  // namespace jit
+}  // namespace rsgpu

@@ -19,6 +19,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
 #include <utility>
 
 #include "bitslice.h"
@@ -94,25 +95,27 @@ __device__ __forceinline__ void read_slot(uint32_t (&W)[8])
 // and generated code alone.  (Holding the block's row pointers in VGPRs and
 // reading them with v_readlane instead of scalar loads measured slower:
 // 26.3 vs 25.1 ms at C3, tools/jit_profile.)
-template <int NW>
+// SH: one program shared by every block (the GENERATED encode; a distinct
+// symbol, so profiles tell it from the per-block decode)
+template <int NW, bool SH>
 __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_num_vgpr(64))) void k_rs_jit(JitArgs a)
 {
     __shared__ uint4 lds[2][C * 2 * 64];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     const int b = blockIdx.y;
-    if (a.status[b] != 0)
+    if (a.status && a.status[b] != 0)
         return;  // uniform per workgroup: the whole block is skipped
     const int k = a.k;
     const int nch = (k + C - 1) / C;
     const long long tile = blockIdx.x;
     const uint8_t* const* srcs = a.srcs + (size_t)b * k;
-    uint8_t* const* dsts = a.dsts + (size_t)b * a.rows;
+    uint8_t* const* dsts = a.dsts + (size_t)b * a.dst_stride;
     // this wave's generated code: chunk ch at code + ch * stride
 #ifndef RSGPU_JIT_SHARE
-    const uint8_t* code = a.code + ((size_t)b * NW + wave) * (size_t)nch * a.chunk_stride;
+    const uint8_t* code = a.code + (SH ? 0 : (size_t)b * a.block_stride) + (size_t)wave * nch * a.chunk_stride;
 #else  // timing-only builds of tools/jit_profile: 1 = every wave runs wave 0's code, 2 = block 0's too
-    const uint8_t* code = a.code + (size_t)(RSGPU_JIT_SHARE == 2 ? 0 : b) * NW * (size_t)nch * a.chunk_stride;
+    const uint8_t* code = a.code + (size_t)(RSGPU_JIT_SHARE == 2 ? 0 : b) * a.block_stride;
 #endif
     const uint32_t m4 = vconst(0x0F0F0F0Fu), m2 = vconst(0x33333333u), m1 = vconst(0x55555555u);
     const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint4*)&lds[0][0];
@@ -298,17 +301,39 @@ hipError_t launch_jit_emit(int k, int e, long long blocks, const uint8_t* coef, 
     return hipGetLastError();
 }
 
+__global__ void k_jit_copy(uint64_t* dst, const uint64_t* src, long long n)
+{
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (long long)gridDim.x * blockDim.x)
+        dst[i] = src[i];
+}
+
+hipError_t launch_jit_copy(void* dst, const void* src, size_t bytes, hipStream_t st)
+{
+    if (bytes % 8)
+        return hipErrorInvalidValue;
+    const long long n = (long long)(bytes / 8);
+    const unsigned grid = (unsigned)std::min<long long>(1024, (n + 255) / 256);
+    hipLaunchKernelGGL(k_jit_copy, dim3(grid), dim3(256), 0, st, (uint64_t*)dst, (const uint64_t*)src, n);
+    return hipGetLastError();
+}
+
 hipError_t launch_rs_jit(const JitArgs& a, long long blocks, hipStream_t st)
 {
-    if (a.rows <= 0 || a.rows > 32 || a.k <= 0 || !a.code || !a.status)
+    if (a.rows <= 0 || a.rows > 32 || a.dst_stride < a.rows || a.k <= 0 || !a.code || a.chunk_stride <= 0)
         return hipErrorInvalidValue;
     const int nw = (a.rows + 7) / 8;
     dim3 grid((unsigned)((a.len + 2047) / 2048), (unsigned)blocks);
-    switch (nw) {
-    case 1: hipLaunchKernelGGL(jitk::k_rs_jit<1>, grid, dim3(64), 0, st, a); break;
-    case 2: hipLaunchKernelGGL(jitk::k_rs_jit<2>, grid, dim3(128), 0, st, a); break;
-    case 3: hipLaunchKernelGGL(jitk::k_rs_jit<3>, grid, dim3(192), 0, st, a); break;
-    default: hipLaunchKernelGGL(jitk::k_rs_jit<4>, grid, dim3(256), 0, st, a); break;
+    const bool sh = a.block_stride == 0;
+    switch (nw * 2 + (sh ? 1 : 0)) {
+    case 2: hipLaunchKernelGGL((jitk::k_rs_jit<1, false>), grid, dim3(64), 0, st, a); break;
+    case 3: hipLaunchKernelGGL((jitk::k_rs_jit<1, true>), grid, dim3(64), 0, st, a); break;
+    case 4: hipLaunchKernelGGL((jitk::k_rs_jit<2, false>), grid, dim3(128), 0, st, a); break;
+    case 5: hipLaunchKernelGGL((jitk::k_rs_jit<2, true>), grid, dim3(128), 0, st, a); break;
+    case 6: hipLaunchKernelGGL((jitk::k_rs_jit<3, false>), grid, dim3(192), 0, st, a); break;
+    case 7: hipLaunchKernelGGL((jitk::k_rs_jit<3, true>), grid, dim3(192), 0, st, a); break;
+    case 8: hipLaunchKernelGGL((jitk::k_rs_jit<4, false>), grid, dim3(256), 0, st, a); break;
+    default: hipLaunchKernelGGL((jitk::k_rs_jit<4, true>), grid, dim3(256), 0, st, a); break;
     }
     return hipGetLastError();
 }

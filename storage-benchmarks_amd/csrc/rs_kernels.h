@@ -94,12 +94,15 @@ hipError_t launch_decode_prepare_syn(int k, int e, long long blocks, const uint8
 // The one-matrix decode through generated code (rs_jit.hip).
 struct JitArgs {
     const uint8_t* const* srcs;      // [B][k]
-    uint8_t* const* dsts;            // [B][rows]
-    const uint8_t* code;             // executable, written by k_jit_emit
-    long long chunk_stride;          // jit::chunk_stride(8)
+    uint8_t* const* dsts;            // [B][dst_stride], this launch's rows first
+    const uint8_t* code;             // executable: block b, wave w, chunk ch at
+                                     // code + b block_stride + (w nch + ch) chunk_stride
+    long long chunk_stride;          // jit::chunk_stride(8), or jit::host_chunk_stride()
+    long long block_stride;          // bytes; 0 = one program shared by every block
     int k, rows;                     // rows <= 32
+    int dst_stride;                  // output pointers per block (>= rows)
     long long len;                   // % 32 == 0
-    const int* status;               // [B]
+    const int* status;               // [B] or nullptr (every block runs)
 };
 size_t jit_code_bytes(int k, int e, long long blocks);
 // k_rs_jit's straight-line code (rs_jit.h) for every (block, wave, chunk) at
@@ -109,6 +112,9 @@ hipError_t launch_jit_emit(int k, int e, long long blocks, const uint8_t* coef, 
                            uint8_t* code, hipStream_t st);
 hipError_t launch_jit_fill(void* code, size_t bytes, hipStream_t st);
 hipError_t launch_rs_jit(const JitArgs& a, long long blocks, hipStream_t st);
+// device-to-device copy into executable memory (host-built code staged in
+// ordinary device memory first), bytes % 8 == 0
+hipError_t launch_jit_copy(void* dst, const void* src, size_t bytes, hipStream_t st);
 
 // Threaded-code bit-sliced dot product with runtime coefficients (rs_tc.hip):
 // dsts[b][i] = sum_p c_b[i][p] * srcs[b][p] for rows <= 32 per launch, where

@@ -14,6 +14,7 @@
 
 #include "../../include/rsgpu.h"
 #include "gf256.h"
+#include "jit_prog.h"
 #include "rs_jit.h"
 #include "rs_kernels.h"
 #include "rs_synth.h"
@@ -37,6 +38,16 @@ struct rsgpu_ctx {
     size_t jit_bytes = 0;
     int jit_state = 0;
     hsa_amd_memory_pool_t jit_pool{};
+    // host-built code of the last shared coefficient matrix (jit_prog.h):
+    // executable copy, its key (k, rows, coefficients) and chunk stride, and
+    // the ordinary device buffer it is staged through
+    int encode_kernel = RSGPU_ENCODE_AUTO;
+    void* d_enc_code = nullptr;
+    size_t enc_code_bytes = 0;
+    std::vector<uint8_t> enc_key;
+    int enc_chunk_stride = 0;
+    void* d_code_stage = nullptr;
+    size_t code_stage_bytes = 0;
     std::string err;
     // grow-only device scratch for pointer tables / coefficient tables
     void* d_scratch = nullptr;
@@ -308,6 +319,85 @@ int jit_ensure(rsgpu_ctx* ctx, size_t bytes)
     return RSGPU_OK;
 }
 
+// The generated code of coefficient matrix coef[rows][k] shared by every
+// block (jit_prog.h) in ctx->d_enc_code; rebuilt only when the matrix
+// changes.  Stream-ordered: the copy into the executable buffer runs after
+// every kernel enqueued before it, which may still run the old program.
+int shared_program(rsgpu_ctx* ctx, const uint8_t* coef, int k, int rows)
+{
+    std::vector<uint8_t> key(8 + (size_t)k * rows);
+    std::memcpy(key.data(), &k, 4);
+    std::memcpy(key.data() + 4, &rows, 4);
+    std::memcpy(key.data() + 8, coef, (size_t)k * rows);
+    if (ctx->d_enc_code && key == ctx->enc_key)
+        return RSGPU_OK;
+    if (jit_probe(ctx) != 1)
+        return fail(ctx, RSGPU_ERR_UNSUPPORTED, "no executable device memory pool");
+    int stride = 0;
+    const std::vector<uint8_t> code = jit::build_matrix_code(coef, k, rows, &stride);
+    if (ctx->enc_code_bytes < code.size()) {
+        RS_HIP(ctx, hipStreamSynchronize(ctx->stream));
+        if (ctx->d_enc_code)
+            hsa_amd_memory_pool_free(ctx->d_enc_code);
+        ctx->d_enc_code = nullptr;
+        ctx->enc_code_bytes = 0;
+        void* p = nullptr;
+        if (hsa_amd_memory_pool_allocate(ctx->jit_pool, code.size(), HSA_AMD_MEMORY_POOL_EXECUTABLE_FLAG,
+                                         &p) != HSA_STATUS_SUCCESS || !p)
+            return fail(ctx, RSGPU_ERR_NOMEM, "executable device allocation failed");
+        ctx->d_enc_code = p;
+        ctx->enc_code_bytes = code.size();
+    }
+    if (ctx->code_stage_bytes < code.size()) {
+        RS_HIP(ctx, hipStreamSynchronize(ctx->stream));
+        if (ctx->d_code_stage)
+            RS_HIP(ctx, hipFree(ctx->d_code_stage));
+        ctx->d_code_stage = nullptr;
+        RS_HIP(ctx, hipMalloc(&ctx->d_code_stage, code.size()));
+        ctx->code_stage_bytes = code.size();
+    }
+    void* stage;
+    int rc = get_stage(ctx, code.size(), &stage);
+    if (rc)
+        return rc;
+    std::memcpy(stage, code.data(), code.size());
+    rc = upload(ctx, ctx->d_code_stage, code.size());
+    if (rc)
+        return rc;
+    RS_HIP(ctx, launch_jit_copy(ctx->d_enc_code, ctx->d_code_stage, code.size(), ctx->stream));
+    ctx->enc_key = key;
+    ctx->enc_chunk_stride = stride;
+    return RSGPU_OK;
+}
+
+// dsts[b][i] = sum_j coef[i][j] srcs[b][j] through the shared generated code,
+// in passes of <= 32 rows (aligned rows, len % 32 == 0)
+int shared_program_launch(rsgpu_ctx* ctx, const uint8_t* coef, int k, int rows, long long len,
+                          long long blocks, const uint8_t* const* d_srcs, uint8_t* const* d_dsts,
+                          const char* name)
+{
+    int rc = shared_program(ctx, coef, k, rows);
+    if (rc)
+        return rc;
+    const int nch = (k + 7) / 8;
+    for (int p = 0; p * 32 < rows; ++p) {
+        JitArgs j{};
+        j.srcs = d_srcs;
+        j.dsts = d_dsts + 32 * p;
+        j.code = (const uint8_t*)ctx->d_enc_code + (size_t)p * 4 * nch * ctx->enc_chunk_stride;
+        j.chunk_stride = ctx->enc_chunk_stride;
+        j.block_stride = 0;
+        j.k = k;
+        j.rows = std::min(32, rows - 32 * p);
+        j.dst_stride = rows;
+        j.len = len;
+        j.status = nullptr;
+        KTimer kt(ctx, name, (size_t)blocks);
+        RS_HIP(ctx, launch_rs_jit(j, blocks, ctx->stream));
+    }
+    return RSGPU_OK;
+}
+
 // Host-side handler addresses of coefficient matrix coef[rows][k] in the
 // pass layout (rs_kernels.h tc_elem): pass p, source j, slot s -> row 32p + s.
 void tc_fill_addr(const rsgpu_ctx* ctx, const uint8_t* coef, int k, int rows, unsigned long long* h)
@@ -375,10 +465,23 @@ int rows_pad_for(int rows)
 // of scratch in the same upload (the pointer tables of ec_encode_data).
 int dot_from_host_coef(rsgpu_ctx* ctx, const uint8_t* coef, int k, int rows, long long len,
                        long long blocks, const uint8_t* const* d_srcs, uint8_t* const* d_dsts,
-                       size_t tab_off, bool aligned, const char* tc_name,
+                       size_t tab_off, bool aligned, const char* tc_name, const char* jit_name,
                        const void* pre = nullptr, size_t pre_bytes = 0)
 {
     const bool tcp = aligned && len % 32 == 0 && tc_ready(ctx);
+    if (aligned && len % 32 == 0 && ctx->encode_kernel != RSGPU_ENCODE_THREADED && jit_probe(ctx) == 1) {
+        if (pre) {  // the row pointers the caller staged with the table upload
+            void* stage;
+            int rc = get_stage(ctx, pre_bytes, &stage);
+            if (rc)
+                return rc;
+            std::memcpy(stage, pre, pre_bytes);
+            rc = upload(ctx, ctx->d_scratch, pre_bytes);
+            if (rc)
+                return rc;
+        }
+        return shared_program_launch(ctx, coef, k, rows, len, blocks, d_srcs, d_dsts, jit_name);
+    }
     const int rows_pad = rows_pad_for(rows);
     const size_t n = (size_t)k * rows_pad;
     const size_t bytes = tcp ? sizeof(unsigned long long) * (size_t)tc_table_elems(k, rows)
@@ -479,6 +582,10 @@ int rsgpu_destroy(rsgpu_ctx* ctx)
         (void)hipFree(ctx->d_tc_table);
     if (ctx->d_jit)
         hsa_amd_memory_pool_free(ctx->d_jit);
+    if (ctx->d_enc_code)
+        hsa_amd_memory_pool_free(ctx->d_enc_code);
+    if (ctx->d_code_stage)
+        (void)hipFree(ctx->d_code_stage);
     delete ctx;
     return RSGPU_OK;
 }
@@ -704,7 +811,8 @@ int rsgpu_ec_encode_data(rsgpu_ctx* ctx, int len, int k, int rows, const unsigne
     char* d = (char*)ctx->d_scratch;
     return dot_from_host_coef(ctx, coef.data(), k, rows, len, 1, (const uint8_t* const*)d,
                               (uint8_t* const*)(d + sizeof(void*) * k), ptr_bytes, aligned,
-                              "k_rs_tc(ec_encode_data)", hp.data(), sizeof(void*) * hp.size());
+                              "k_rs_tc(ec_encode_data)", "k_rs_jit(ec_encode_data)", hp.data(),
+                              sizeof(void*) * hp.size());
 }
 
 int rsgpu_ec_encode_data_update(rsgpu_ctx* ctx, int len, int k, int rows, int vec_i,
@@ -784,13 +892,15 @@ int rsgpu_encode_blocks(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch, 
                          (pitch % 16 == 0);
     // Fast paths: the gf_gen_rs_matrix code with compile-time coefficients,
     // bit-sliced (len % 32 == 0) or nibble-table (len % 4 == 0).
-    if (!coef && aligned && len % 32 == 0 && rs_bitsliced_available(k, e)) {
+    const bool compiled_ok = ctx->encode_kernel == RSGPU_ENCODE_AUTO || ctx->encode_kernel == RSGPU_ENCODE_COMPILED;
+    if (compiled_ok && !coef && aligned && len % 32 == 0 && rs_bitsliced_available(k, e)) {
         KTimer kt(ctx, "k_rs_bs(encode)", blocks);
         RS_HIP(ctx, launch_rs_bitsliced(k, e, d_src, d_parity, (long long)pitch, (long long)len,
                                         (long long)blocks, ctx->stream));
         return RSGPU_OK;
     }
-    if (!coef && aligned && len % 4 == 0 && rs_encode_specialized_available(k, e)) {
+    if (compiled_ok && !coef && aligned && len % 4 == 0 && len % 32 != 0 &&
+        rs_encode_specialized_available(k, e)) {
         KTimer kt(ctx, "k_rs_encode_lh", blocks);
         RS_HIP(ctx, launch_rs_encode_specialized(k, e, d_src, d_parity, (long long)pitch,
                                                  (long long)len, (long long)blocks, ctx->stream));
@@ -816,7 +926,16 @@ int rsgpu_encode_blocks(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch, 
                                 (const uint8_t**)(d + src_ptr_bytes), ctx->stream));
     return dot_from_host_coef(ctx, c.data(), k, e, (long long)len, (long long)blocks,
                               (const uint8_t* const*)d, (uint8_t* const*)(d + src_ptr_bytes),
-                              src_ptr_bytes + dst_ptr_bytes, aligned, "k_rs_tc(encode)");
+                              src_ptr_bytes + dst_ptr_bytes, aligned, "k_rs_tc(encode)",
+                              "k_rs_jit(encode)");
+}
+
+int rsgpu_set_encode_kernel(rsgpu_ctx* ctx, int kernel)
+{
+    if (!ctx || kernel < RSGPU_ENCODE_AUTO || kernel > RSGPU_ENCODE_THREADED)
+        return fail(ctx, RSGPU_ERR_ARG, "rsgpu_set_encode_kernel: unknown kernel");
+    ctx->encode_kernel = kernel;
+    return RSGPU_OK;
 }
 
 int rsgpu_set_decode_kernel(rsgpu_ctx* ctx, int kernel)
@@ -1054,8 +1173,10 @@ int rsgpu_decode_apply(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch, s
         j.dsts = (uint8_t* const*)(ws + w.outp);
         j.code = (const uint8_t*)ctx->d_jit;
         j.chunk_stride = jit::chunk_stride(8);
+        j.block_stride = (long long)((e + 7) / 8) * ((k + 7) / 8) * jit::chunk_stride(8);
         j.k = k;
         j.rows = e;
+        j.dst_stride = e;
         j.len = (long long)len;
         j.status = d_status;
         KTimer kt(ctx, "k_rs_jit(decode)", blocks);
@@ -1202,6 +1323,21 @@ int rsgpu_fill_synthetic(rsgpu_ctx* ctx, unsigned char* d_rows, size_t rows, siz
     RS_HIP(ctx, launch_fill_synth(d_rows, (long long)rows, (long long)len, (long long)pitch, seed,
                                   row0, ctx->stream));
     return RSGPU_OK;
+}
+
+// Test hook (not in include/rsgpu.h): the host-built code of an e x k matrix
+// shared by every block (jit_prog.h, the GENERATED encode), for the CPU
+// suite to disassemble and interpret.  Returns the bytes needed, or -1;
+// writes only when out_bytes is large enough; *chunk_stride gets the stride.
+long long rsgpu_internal_jit_matrix_code(int k, int e, const unsigned char* coef, unsigned char* out,
+                                         size_t out_bytes, int* chunk_stride)
+{
+    if (k <= 0 || k > 250 || e <= 0 || e > 255 || !coef || !chunk_stride)
+        return -1;
+    const std::vector<uint8_t> code = jit::build_matrix_code(coef, k, e, chunk_stride);
+    if (out && out_bytes >= code.size())
+        std::memcpy(out, code.data(), code.size());
+    return (long long)code.size();
 }
 
 // Test hook (not part of include/rsgpu.h): the generated decode code of ONE

@@ -47,6 +47,8 @@ ERRORS = {-1: "RSGPU_ERR_ARG", -2: "RSGPU_ERR_HIP", -3: "RSGPU_ERR_SINGULAR",
 MAX_SOURCES = 250  # TEST_SOURCES, isa.cpp:25-27
 # rsgpu_set_decode_kernel choices (include/rsgpu.h)
 DECODE_KERNELS = {"auto": 0, "one_matrix": 1, "fused": 2, "general": 3, "generated": 4}
+# rsgpu_set_encode_kernel choices (include/rsgpu.h)
+ENCODE_KERNELS = {"auto": 0, "compiled": 1, "generated": 2, "threaded": 3}
 
 vp = C.c_void_p
 sz = C.c_size_t
@@ -81,6 +83,7 @@ _SIGS = {
     "rsgpu_encode_blocks": (C.c_int, [vp, C.c_int, C.c_int, sz, sz, sz, vp, vp, vp]),
     "rsgpu_decode_workspace_bytes": (sz, [C.c_int, C.c_int, sz]),
     "rsgpu_set_decode_kernel": (C.c_int, [vp, C.c_int]),
+    "rsgpu_set_encode_kernel": (C.c_int, [vp, C.c_int]),
     "rsgpu_decode_general_workspace_bytes": (sz, [C.c_int, C.c_int, C.c_int, sz]),
     "rsgpu_decode_general": (C.c_int, [vp, C.c_int, C.c_int, sz, sz, sz, vp, vp, vp, vp, C.c_int,
                                        vp, vp, vp]),
@@ -227,6 +230,12 @@ class Context:
     def set_torch_stream(self) -> None:
         import torch
         self.set_stream(torch.cuda.current_stream().cuda_stream)
+
+    def set_encode_kernel(self, kernel: str) -> None:
+        """Encode kernel of encode_blocks / ec_encode_data: auto | compiled |
+        generated | threaded (include/rsgpu.h rsgpu_set_encode_kernel)."""
+        self.check(lib().rsgpu_set_encode_kernel(self._h, ENCODE_KERNELS[kernel]),
+                   "rsgpu_set_encode_kernel")
 
     def set_decode_kernel(self, kernel: str) -> None:
         """Decode kernel of decode_blocks: auto | one_matrix | fused | general

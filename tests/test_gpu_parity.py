@@ -356,9 +356,13 @@ def test_runtime_coefficient_encode_tc(ctx, orc, k, e, L, B, kind):
             assert (got[p] == ref[p]).all(), (blk, p)
 
 
-def test_ec_encode_data_pointer_api_tc(ctx, orc):
+@pytest.mark.parametrize("kernel,name", [("auto", "k_rs_jit(ec_encode_data)"),
+                                         ("threaded", "k_rs_tc(ec_encode_data)")])
+def test_ec_encode_data_pointer_api_tc(ctx, orc, kernel, name):
     """rsgpu_ec_encode_data with 32-multiple lengths and aligned rows takes the
-    threaded-code kernel; same bytes as ec_encode_data_base."""
+    generated code (default) or the threaded-code kernel; same bytes as
+    ec_encode_data_base."""
+    ctx.set_encode_kernel(kernel)
     rng = np.random.default_rng(77)
     k, rows, length = 17, 11, 32 * 1001
     coef = rng.integers(0, 256, (rows, k), dtype=np.uint8)
@@ -371,7 +375,8 @@ def test_ec_encode_data_pointer_api_tc(ctx, orc):
     ctx.ec_encode_data(length, k, rows, g, d_data, d_out)
     names = [n for n, _, _ in ctx.timing_read()]
     ctx.timing_enable(False)
-    assert names == ["k_rs_tc(ec_encode_data)"], names
+    ctx.set_encode_kernel("auto")
+    assert names == [name], names
     ref = [np.zeros(length, np.uint8) for _ in range(rows)]
     orc.encode_data(length, k, rows, g, data, ref)
     for r in range(rows):

@@ -154,3 +154,81 @@ def test_layout_independent_of_coefficients():
         ins = disasm(emit(k, e, coef).tobytes())
         layouts.append([(off, m.startswith("v_") and m != "ds_read_b128") for off, m, _ in ins])
     assert layouts[0] == layouts[1] == layouts[2]
+
+
+def matrix_code(k, e, coef):
+    import rsgpu
+    f = rsgpu.lib().rsgpu_internal_jit_matrix_code
+    f.restype = C.c_longlong
+    f.argtypes = [C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_size_t, C.POINTER(C.c_int)]
+    coef = np.ascontiguousarray(coef, np.uint8)
+    stride = C.c_int()
+    need = f(k, e, coef.ctypes.data, None, 0, C.byref(stride))
+    out = np.zeros(need, np.uint8)
+    assert f(k, e, coef.ctypes.data, out.ctypes.data, need, C.byref(stride)) == need
+    return out.tobytes(), stride.value
+
+
+def rs_rows(k, e):
+    """gf_gen_rs_matrix rows k..k+e-1 (isa/ec_base.c:62-79): 2^(r j)."""
+    rows = []
+    for r in range(e):
+        gen, p, row = 1, 1, []
+        for _ in range(r):
+            gen = g.gf_mul(gen, 2)
+        for _ in range(k):
+            row.append(p)
+            p = g.gf_mul(p, gen)
+        rows.append(row)
+    return np.array(rows, np.uint8)
+
+
+@pytest.mark.parametrize("k,e,kind", [(64, 32, "rs"), (32, 16, "random"), (128, 64, "random"),
+                                      (20, 13, "random"), (9, 40, "random"), (100, 20, "rs")])
+def test_shared_matrix_code(k, e, kind):
+    """The GENERATED encode's host-built code (jit_prog.cpp): per (wave,
+    source) only the composites a greedy cover needs, rows in passes of 32.
+    Interpreted chunk by chunk, every accumulator must equal sum_q c[row][q]
+    * src_q over GF(2^8); every register read after its LDS load was waited
+    for; and the composites must average well under the 22 of the full
+    tables."""
+    rng = random.Random(k * 1000 + e)
+    if kind == "rs":
+        coef = rs_rows(k, e)
+    else:
+        coef = np.array([[rng.randrange(256) for _ in range(k)] for _ in range(e)], np.uint8)
+        coef[0, 0] = 0
+    code, stride = matrix_code(k, e, coef)
+    nch = (k + 7) // 8
+    assert len(code) == ((e + 31) // 32) * 4 * nch * stride
+    src = [[rng.randrange(256) for _ in range(32)] for _ in range(k)]
+    n_comp = n_src = 0
+    for p in range((e + 31) // 32):
+        prow = min(32, e - 32 * p)
+        for w in range((prow + 7) // 8):
+            regs = {r: 0 for r in range(256)}
+            pending = []
+            for ch in range(nch):
+                base = ((p * 4 + w) * nch + ch) * stride
+                nt = min(8, k - 8 * ch)
+                ins = disasm(code[base:base + stride])
+                end = next(off for off, m, _ in ins if m == "s_setpc_b64")
+                ins = [x for x in ins if x[0] <= end]
+                n_comp += sum(1 for off, m, ops in ins if m in ("v_xor_b32_e32", "v_bitop3_b32")
+                              and int(regs_of(ops.split(",")[0])[0]) < 64)
+                n_src += nt
+                lds = {}
+                for t in range(nt):
+                    pl = planes(src[8 * ch + t])
+                    for a in range(8):
+                        lds[t * 2048 + (a // 4) * 1024 + 4 * (a % 4)] = pl[a]
+                run_chunk(ins, regs, lds, pending)
+                assert not pending, "a load left outstanding at the return"
+            for s in range(min(8, prow - 8 * w)):
+                row = 32 * p + 8 * w + s
+                want = [0] * 32
+                for q in range(k):
+                    want = [x ^ g.gf_mul(int(coef[row, q]), y) for x, y in zip(want, src[q])]
+                got = unplanes([regs[64 + 8 * s + b] for b in range(8)])
+                assert got == want, (k, e, row)
+    assert n_comp / n_src < 18, n_comp / n_src

@@ -136,6 +136,8 @@ int main(int argc, char** argv)
     a.dsts = d_dp;
     a.code = (const uint8_t*)exec;
     a.chunk_stride = (long long)stride;
+    a.block_stride = (long long)NW * nch * stride;
+    a.dst_stride = e;
     a.k = k;
     a.rows = e;
     a.len = L;
@@ -148,7 +150,7 @@ int main(int argc, char** argv)
         (void)hipEventCreate(&e1);
         (void)hipEventRecord(e0);
         if (extra_lds && e > 24)
-            hipLaunchKernelGGL(jitk::k_rs_jit<4>, dim3((unsigned)((L + 2047) / 2048), (unsigned)B), dim3(256),
+            hipLaunchKernelGGL((jitk::k_rs_jit<4, false>), dim3((unsigned)((L + 2047) / 2048), (unsigned)B), dim3(256),
                                extra_lds, 0, a);
         else
             (void)launch_rs_jit(a, B, 0);

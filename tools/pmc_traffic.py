@@ -19,7 +19,7 @@ def name_of(kernel: str) -> str:
     if "k_rs_decode_fused" in kernel:
         return "k_rs_decode_fused"
     if "k_rs_jit" in kernel:
-        return "k_rs_jit(decode)"
+        return "k_rs_jit(encode)" if "true>" in kernel.split("(")[0] else "k_rs_jit(decode)"
     if "k_rs_tc" in kernel:  # the bench's only k_rs_tc launch is the one-matrix decode
         return "k_rs_tc(decode)"
     if "k_dot_generic" in kernel:
