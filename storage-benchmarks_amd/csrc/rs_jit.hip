@@ -103,12 +103,22 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_num_vgpr(64))) void 
     __shared__ uint4 lds[2][C * 2 * 64];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
-    const int b = blockIdx.y;
+    int b = blockIdx.y;
+    long long tile = blockIdx.x;
+    if (a.xcd_order) {
+        // workgroups are dealt round-robin over the 8 XCDs: give each XCD a
+        // contiguous range of (block, tile), so all tiles of a block (and its
+        // code) stay in one XCD's L2 -- it matters when a block has few tiles
+        const unsigned g = blockIdx.x + gridDim.x * blockIdx.y, tot = gridDim.x * gridDim.y;
+        const unsigned xcd = g & 7, q8 = tot >> 3, r8 = tot & 7;
+        const unsigned lin = xcd * q8 + min(xcd, r8) + (g >> 3);
+        b = (int)(lin / gridDim.x);
+        tile = lin - (unsigned)b * gridDim.x;
+    }
     if (a.status && a.status[b] != 0)
         return;  // uniform per workgroup: the whole block is skipped
     const int k = a.k;
     const int nch = (k + C - 1) / C;
-    const long long tile = blockIdx.x;
     const uint8_t* const* srcs = a.srcs + (size_t)b * k;
     uint8_t* const* dsts = a.dsts + (size_t)b * a.dst_stride;
     // this wave's generated code: chunk ch at code + ch * stride

@@ -103,6 +103,7 @@ struct JitArgs {
     int dst_stride;                  // output pointers per block (>= rows)
     long long len;                   // % 32 == 0
     const int* status;               // [B] or nullptr (every block runs)
+    int xcd_order;                   // non-zero: XCD-contiguous (block, tile) order
 };
 size_t jit_code_bytes(int k, int e, long long blocks);
 // k_rs_jit's straight-line code (rs_jit.h) for every (block, wave, chunk) at

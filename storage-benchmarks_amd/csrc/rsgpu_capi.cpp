@@ -960,8 +960,10 @@ enum class Plan {
     general_dot  // k_decode_prepare + k_dot_generic (unaligned / odd lengths)
 };
 
-// column tiles (2 KB) per block from which AUTO decodes through generated code
-constexpr size_t kJitMinTiles = 128;
+// column tiles (2 KB) per block from which AUTO decodes through generated
+// code; below kJitXcdTiles the decode runs in XCD-contiguous order
+constexpr size_t kJitMinTiles = 48;
+constexpr size_t kJitXcdTiles = 128;
 
 bool rows_aligned(size_t len, size_t pitch, const void* a, const void* b, const void* c)
 {
@@ -983,8 +985,9 @@ Plan decode_plan(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch, const v
         return Plan::one_matrix;
     // AUTO: generated code only when a block has enough column tiles to
     // amortise its ~160 KB of code (every tile's workgroup fetches all of
-    // it): C3 / C5 (489 tiles) 25.2 / 15.0 ms vs 27 / 17.7 threaded; C4
-    // (16 tiles) 16.6 + 4.7 prepare vs 14.9 + 0.4 (profiles/r02_ab)
+    // it): C3 / C5 (489 tiles) 25.2 / 15.0 ms vs 27 / 17.7 threaded; L =
+    // 128000 (63 tiles) 3.79 vs 3.94 ms; C4 (16 tiles) 14.7 + 1.25 emission
+    // vs 15.0 per 16384 blocks (profiles/r02_ab)
     if (want == RSGPU_DECODE_AUTO && (len + 2047) / 2048 < kJitMinTiles)
         return Plan::one_matrix;
     return Plan::generated;
@@ -1179,6 +1182,8 @@ int rsgpu_decode_apply(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch, s
         j.dst_stride = e;
         j.len = (long long)len;
         j.status = d_status;
+        // few tiles per block: keep each block's code in one XCD's L2
+        j.xcd_order = (len + 2047) / 2048 < kJitXcdTiles;
         KTimer kt(ctx, "k_rs_jit(decode)", blocks);
         RS_HIP(ctx, launch_rs_jit(j, (long long)blocks, ctx->stream));
         return RSGPU_OK;
