@@ -38,7 +38,7 @@ int main(int argc, char** argv)
                             hipMemcpyDeviceToDevice);
         (void)hipFree(d);
     }
-    auto run = [&] { return launch_rs_bitsliced(k, e, src, nullptr, out, pitch, L, B, nullptr, 0); };
+    auto run = [&] { return launch_rs_bitsliced(k, e, src, out, pitch, L, B, 0); };
     (void)run();
     (void)run();
     if (hipDeviceSynchronize() != hipSuccess) {

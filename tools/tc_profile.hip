@@ -77,10 +77,9 @@ int main(int argc, char** argv)
     unsigned long long prof[8];
     (void)hipMemcpyFromSymbol(prof, HIP_SYMBOL(tc::rsgpu_tc_prof), sizeof prof);
     const double waves = (double)(((L + 2047) / 2048 + 63) / 64) * B * (slots / 8);  // sampled WGs
-    // RSGPU_TC_ONEBAR: phase 0 is the wait, phase 1 empty, phase 3 the barrier plus the next issue
-    const char* names[8] = {RSGPU_TC_ONEBAR ? "wait vmcnt" : "issue DMA", RSGPU_TC_ONEBAR ? "-" : "wait vmcnt",
-                            "transpose in", RSGPU_TC_ONEBAR ? "barrier + issue DMA" : "barrier 1",
-                            "chunk asm", "store out", RSGPU_TC_ONEBAR ? "loop" : "barrier 2 + loop", "wave lifetime"};
+    // one barrier per step: phase 0 is the wait, phase 1 empty, phase 3 the barrier plus the next issue
+    const char* names[8] = {"wait vmcnt", "-", "transpose in", "barrier + issue DMA",
+                            "chunk asm", "store out", "loop", "wave lifetime"};
     printf("k_rs_tc<%d>: B=%d k=%d rows=%d L=%lld  %.3f ms  (%.1f GB/s alg)\n", slots / 8, B, k, nrows,
            L, ms, (double)(k + nrows) * L * B / (ms * 1e-3) / 1e9);
     for (int i = 0; i < 8; ++i)
