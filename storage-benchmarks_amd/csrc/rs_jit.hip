@@ -304,7 +304,7 @@ hipError_t launch_jit_fill(void* code, size_t bytes, hipStream_t st)
 hipError_t launch_jit_emit(int k, int e, long long blocks, const uint8_t* coef, const int* status,
                            uint8_t* code, hipStream_t st)
 {
-    if (k <= 0 || k > 250 || e <= 0 || e > 32 || blocks <= 0 || !coef || !status || !code)
+    if (k <= 0 || k > 250 || e <= 0 || k + e > 250 || blocks <= 0 || !coef || !status || !code)
         return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_jit_emit, dim3((unsigned)((e + 7) / 8), (unsigned)blocks), dim3(256), 0, st, k, e,
                        coef, status, code);

@@ -43,6 +43,9 @@ struct PrepArgs {
     const unsigned long long* tc_table = nullptr;
     unsigned long long* tc_addr = nullptr;
     long long tc_block_stride = 0;
+    // or (when non-null) the decode rows themselves, [blocks][nerrs][k], for
+    // k_jit_emit
+    uint8_t* coef_out = nullptr;
 };
 
 int generic_rows_per_pass(int rows);

@@ -539,6 +539,14 @@ __global__ __launch_bounds__(256) void k_decode_prepare(PrepArgs a)
             s ^= gmul(Dm[q * k + j], enc(r, q));
         return s;
     };
+    if (a.coef_out) {
+        uint8_t* cb = a.coef_out + (size_t)b * ne * k;
+        for (int idx = tid; idx < ne * k; idx += nt) {
+            const int i = idx / k, j = idx - i * k;
+            cb[idx] = coef(i, j);
+        }
+        return;
+    }
     if (a.tc_addr && a.tc_table) {
         // k_rs_tc handler addresses (pass layout), padding slots -> handler 0
         unsigned long long* ta = a.tc_addr + (size_t)b * a.tc_block_stride;
@@ -901,7 +909,7 @@ __global__ __launch_bounds__(256) void k_decode_prepare_syn(int k, int e,
                 bad = 1;
             else if (j < 64)
                 m0 |= 1ull << j;
-            else
+            else if (j < 128)  // the bitmask serves the fused kernel (k <= 128) only
                 m1 |= 1ull << (j - 64);
         }
         emask[2 * b] = m0;
@@ -1136,7 +1144,7 @@ hipError_t launch_decode_prepare_syn(int k, int e, long long blocks, const uint8
                                      unsigned long long* dir_addr, uint8_t* jit_coef,
                                      hipStream_t st)
 {
-    if (k <= 0 || k > 250 || e <= 0 || e > 32 ||
+    if (k <= 0 || k > 250 || e <= 0 || e > (jit_coef ? 63 : 32) || k + e > 250 ||
         (!jit_coef && (!tc_table || (!dir_addr && (!tc_addr || !syn_addr)))))
         return hipErrorInvalidValue;
     static bool attr_set = false;

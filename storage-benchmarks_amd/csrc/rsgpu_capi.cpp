@@ -956,8 +956,9 @@ enum class Plan {
     generated,   // k_decode_prepare_syn (closed form, writes code) + k_rs_jit
     one_matrix,  // k_decode_prepare_syn (closed form) + k_rs_tc
     fused,       // k_decode_prepare_syn (e x e) + k_rs_decode_fused
-    general_tc,  // k_decode_prepare (k x k inversion) + k_rs_tc passes
-    general_dot  // k_decode_prepare + k_dot_generic (unaligned / odd lengths)
+    general_tc,   // k_decode_prepare (k x k inversion) + k_rs_tc passes
+    general_jit,  // k_decode_prepare + per-block generated code, passes of 32 rows
+    general_dot   // k_decode_prepare + k_dot_generic (unaligned / odd lengths)
 };
 
 // column tiles (2 KB) per block from which AUTO decodes through generated
@@ -971,14 +972,31 @@ bool rows_aligned(size_t len, size_t pitch, const void* a, const void* b, const 
            (uintptr_t)c % 16 == 0;
 }
 
+// the k x k general decode on aligned rows: generated code where the rows
+// are long enough to amortise it (as decode_plan's AUTO), threaded code else
+Plan general_plan(rsgpu_ctx* ctx, size_t len)
+{
+    if ((len + 2047) / 2048 >= kJitMinTiles && ctx->decode_kernel != RSGPU_DECODE_ONE_MATRIX &&
+        jit_probe(ctx) == 1)
+        return Plan::general_jit;
+    return Plan::general_tc;
+}
+
 Plan decode_plan(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch, const void* src,
                  const void* par, const void* out)
 {
     if (!rows_aligned(len, pitch, src, par, out) || !tc_ready(ctx))
         return Plan::general_dot;
     const int want = ctx->decode_kernel;
+    // the closed-form rows need Lambda's e + 1 coefficients in one wave
+    // (e <= 63); the threaded-code and fused kernels take e <= 32
+    const bool gen_ok = e <= 63 && jit_probe(ctx) == 1 && want != RSGPU_DECODE_ONE_MATRIX &&
+                        want != RSGPU_DECODE_FUSED && want != RSGPU_DECODE_GENERAL &&
+                        (want == RSGPU_DECODE_GENERATED || (len + 2047) / 2048 >= kJitMinTiles);
+    if (e > 32 && gen_ok)
+        return Plan::generated;
     if (want == RSGPU_DECODE_GENERAL || e > 32)
-        return Plan::general_tc;
+        return general_plan(ctx, len);
     if (want == RSGPU_DECODE_FUSED && rs_decode_fused_available(k, e))
         return Plan::fused;
     if (want == RSGPU_DECODE_ONE_MATRIX || jit_probe(ctx) != 1)
@@ -1020,6 +1038,35 @@ WsLayout ws_layout(int k, int e, size_t blocks)
     return w;
 }
 
+// The per-block generated decode (rs_jit.hip) over rows e of every block, in
+// passes of <= 32 rows: block b, pass p, wave w, chunk ch at d_jit + b
+// block_stride + ((4 p + w) nch + ch) chunk_stride (k_jit_emit's layout).
+int jit_decode_launch(rsgpu_ctx* ctx, int k, int e, size_t len, size_t blocks,
+                      const uint8_t* const* d_srcs, uint8_t* const* d_dsts, const int* d_status)
+{
+    if (!ctx->d_jit || ctx->jit_bytes < jit_code_bytes(k, e, (long long)blocks))
+        return fail(ctx, RSGPU_ERR_ARG, "rsgpu_decode_apply: no prepared decode code");
+    const int nch = (k + 7) / 8, nwt = (e + 7) / 8;
+    for (int p = 0; p * 32 < e; ++p) {
+        JitArgs j{};
+        j.srcs = d_srcs;
+        j.dsts = d_dsts + 32 * p;
+        j.code = (const uint8_t*)ctx->d_jit + (size_t)4 * p * nch * jit::chunk_stride(8);
+        j.chunk_stride = jit::chunk_stride(8);
+        j.block_stride = (long long)nwt * nch * jit::chunk_stride(8);
+        j.k = k;
+        j.rows = std::min(32, e - 32 * p);
+        j.dst_stride = e;
+        j.len = (long long)len;
+        j.status = d_status;
+        // few tiles per block: keep each block's code in one XCD's L2
+        j.xcd_order = (len + 2047) / 2048 < kJitXcdTiles;
+        KTimer kt(ctx, "k_rs_jit(decode)", blocks);
+        RS_HIP(ctx, launch_rs_jit(j, (long long)blocks, ctx->stream));
+    }
+    return RSGPU_OK;
+}
+
 // k_decode_prepare launch for the general plans (enc: device m x k matrix
 // or nullptr for gf_gen_rs_matrix)
 int general_prepare(rsgpu_ctx* ctx, Plan plan, int k, int m, int nerrs, bool originals_only,
@@ -1047,7 +1094,12 @@ int general_prepare(rsgpu_ctx* ctx, Plan plan, int k, int m, int nerrs, bool ori
     p.surv_ptrs = (const uint8_t**)(ws + w.surv);
     p.out_ptrs = (uint8_t**)(ws + w.outp);
     p.status = d_status;
-    if (plan == Plan::general_tc) {
+    if (plan == Plan::general_jit) {
+        p.coef_out = (uint8_t*)(ws + w.tab);  // [B][nerrs][k] decode rows
+        const int rc = jit_ensure(ctx, jit_code_bytes(k, nerrs, (long long)blocks));
+        if (rc)
+            return rc;
+    } else if (plan == Plan::general_tc) {
         p.tc_table = ctx->d_tc_table;
         p.tc_addr = (unsigned long long*)(ws + w.tab);
         p.tc_block_stride = tc_table_elems(k, nerrs);
@@ -1056,8 +1108,15 @@ int general_prepare(rsgpu_ctx* ctx, Plan plan, int k, int m, int nerrs, bool ori
         p.ctab = (uint32_t*)(ws + w.tab + sizeof(uint4) * (size_t)k * p.rows_pad * blocks);
         p.tab_block_stride = (long long)k * p.rows_pad;
     }
-    KTimer kt(ctx, "k_decode_prepare", blocks);
-    RS_HIP(ctx, launch_decode_prepare(p, ctx->stream));
+    {
+        KTimer kt(ctx, "k_decode_prepare", blocks);
+        RS_HIP(ctx, launch_decode_prepare(p, ctx->stream));
+    }
+    if (plan == Plan::general_jit) {
+        KTimer ke(ctx, "k_jit_emit", blocks);
+        RS_HIP(ctx, launch_jit_emit(k, nerrs, (long long)blocks, p.coef_out, d_status, (uint8_t*)ctx->d_jit,
+                                    ctx->stream));
+    }
     return RSGPU_OK;
 }
 
@@ -1066,6 +1125,9 @@ int general_apply(rsgpu_ctx* ctx, Plan plan, int k, int nerrs, size_t len, size_
 {
     const WsLayout w = ws_layout(k, nerrs, blocks);
     char* ws = (char*)d_workspace;
+    if (plan == Plan::general_jit)
+        return jit_decode_launch(ctx, k, nerrs, len, blocks, (const uint8_t* const*)(ws + w.surv),
+                                 (uint8_t* const*)(ws + w.outp), d_status);
     if (plan == Plan::general_tc)
         return tc_launch(ctx, "k_rs_tc(decode)", (const uint8_t* const*)(ws + w.surv),
                          (uint8_t* const*)(ws + w.outp), (const unsigned long long*)(ws + w.tab),
@@ -1167,27 +1229,10 @@ int rsgpu_decode_apply(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch, s
     const Plan plan = decode_plan(ctx, k, e, len, pitch, d_src, d_parity, d_out);
     const WsLayout w = ws_layout(k, e, blocks);
     char* ws = (char*)d_workspace;
-    if (plan == Plan::generated) {
-        // one pass, one matrix, the block's generated code (rs_jit.hip)
-        if (!ctx->d_jit || ctx->jit_bytes < jit_code_bytes(k, e, (long long)blocks))
-            return fail(ctx, RSGPU_ERR_ARG, "rsgpu_decode_apply: no prepared decode code");
-        JitArgs j{};
-        j.srcs = (const uint8_t* const*)(ws + w.surv);
-        j.dsts = (uint8_t* const*)(ws + w.outp);
-        j.code = (const uint8_t*)ctx->d_jit;
-        j.chunk_stride = jit::chunk_stride(8);
-        j.block_stride = (long long)((e + 7) / 8) * ((k + 7) / 8) * jit::chunk_stride(8);
-        j.k = k;
-        j.rows = e;
-        j.dst_stride = e;
-        j.len = (long long)len;
-        j.status = d_status;
-        // few tiles per block: keep each block's code in one XCD's L2
-        j.xcd_order = (len + 2047) / 2048 < kJitXcdTiles;
-        KTimer kt(ctx, "k_rs_jit(decode)", blocks);
-        RS_HIP(ctx, launch_rs_jit(j, (long long)blocks, ctx->stream));
-        return RSGPU_OK;
-    }
+    if (plan == Plan::generated)
+        // one matrix, the block's generated code (rs_jit.hip), passes of 32 rows
+        return jit_decode_launch(ctx, k, e, len, blocks, (const uint8_t* const*)(ws + w.surv),
+                                 (uint8_t* const*)(ws + w.outp), d_status);
     if (plan == Plan::one_matrix)
         // one pass, one matrix over the k - e survivors and the e parity rows
         return tc_launch(ctx, "k_rs_tc(decode)", (const uint8_t* const*)(ws + w.surv),
@@ -1268,7 +1313,7 @@ int rsgpu_decode_general(rsgpu_ctx* ctx, int k, int m, size_t len, size_t pitch,
         return RSGPU_OK;
     }
     const bool tcp = rows_aligned(len, pitch, d_src, d_parity, d_out) && tc_ready(ctx);
-    const Plan plan = tcp ? Plan::general_tc : Plan::general_dot;
+    const Plan plan = tcp ? general_plan(ctx, len) : Plan::general_dot;
     const uint8_t* d_enc = nullptr;
     if (encode_matrix) {
         const size_t bytes = (size_t)m * k;

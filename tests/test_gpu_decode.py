@@ -84,7 +84,9 @@ def decode_poisoned(ctx, enc, dec):
 
 GEOMS = [(16, 4, 1000000, 2), (64, 32, 1000000, 2), (100, 20, 1000000, 2), (16, 8, 64000, 4),
          (64, 32, 32000, 16), (40, 20, 8192, 3), (200, 32, 2048, 2), (128, 64, 4096, 2),
-         (12, 12, 512, 2), (33, 1, 64, 2)]
+         (12, 12, 512, 2), (33, 1, 64, 2),
+         # 32 < e <= 63: closed-form rows, generated code in passes of 32 rows
+         (96, 48, 131072, 2), (187, 63, 4096, 2), (40, 33, 98304, 2)]
 
 
 @pytest.mark.parametrize("kernel", KERNELS)
