@@ -1,0 +1,14 @@
+# Geometry sweep at full row length (L = 1e6), AUTO kernels, ~64-96 GB per step:
+#   bash tools/geom_sweep.sh TAG  -> gpurun_out/sweep_TAG/k<K>_l<LOSS>.log
+set -o pipefail
+TAG=${1:-x}
+O=$(pwd)/gpurun_out/sweep_$TAG
+mkdir -p $O
+T="timeout -k 10 200"
+for k in 8 16 32 48 64 100 128 200; do
+  for loss in 0.25 0.5; do
+    B=$(( 96000 / (k * 3 / 2 + 1) ))
+    [ $B -gt 2048 ] && B=2048
+    $T python3 bench.py --no-cpu-baseline --steps 4 --warmup 1 --symbols $k --loss-rate $loss --blocks $B > $O/k${k}_l${loss}.log 2>&1 || exit 1
+  done
+done
