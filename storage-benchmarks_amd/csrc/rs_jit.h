@@ -46,11 +46,7 @@ constexpr int ACC = 64;          // accumulator base register
 constexpr int LDS_SRC = 2048;    // LDS bytes per source: [2 halves][64 lanes] x 16 B
 constexpr int LDS_HALF = 1024;
 constexpr int PRO_BYTES = 16;
-#ifndef RSGPU_JIT_NCOMP
 constexpr int PRE_BYTES = 112;   // per source before the multiply-accumulates
-#else  // timing-only builds (tools/jit_profile): the first RSGPU_JIT_NCOMP composites only
-constexpr int PRE_BYTES = (20 + 4 * RSGPU_JIT_NCOMP + 7) / 8 * 8;
-#endif
 constexpr int EPI_BYTES = 8;
 
 RJ_HD constexpr int src_bytes(int nslot) { return PRE_BYTES + 64 * nslot; }
@@ -112,72 +108,76 @@ RJ_HD inline uint8_t mat_row(uint8_t c, int b)
     return r;
 }
 
-// Output plane b of the multiply-accumulate of coefficient c on slot s, bank
-// `bank` (8 bytes): acc_b ^= L[m_b & 15] ^ H[m_b >> 4], m_b = row b.
-RJ_HD inline uint64_t mac_word(uint8_t c, int s, int b, int bank)
+// The eight words of coefficient c on slot s at once (one matrix per call)
+RJ_HD inline void mac_words(uint8_t c, int s, int bank, uint64_t (&wd)[8])
 {
-    const uint8_t row = mat_row(c, b);
-    const int acc = ACC + 8 * s + b, lo = row & 15, hi = row >> 4;
-    if (lo && hi)
-        return enc_bitop3_96(acc, acc, table_reg(bank, 0, lo), table_reg(bank, 1, hi));
-    if (lo)
-        return enc_xor_e64(acc, acc, table_reg(bank, 0, lo));
-    if (hi)
-        return enc_xor_e64(acc, acc, table_reg(bank, 1, hi));
-    return (uint64_t)S_NOP0 << 32 | S_NOP0;  // c == 0
-}
-
-// Writes the 64 multiply-accumulate bytes of coefficient c on slot s, bank
-// `bank`, at dst (8-byte aligned).
-RJ_HD inline void emit_mac(uint64_t* dst, uint8_t c, int s, int bank)
-{
-    for (int b = 0; b < 8; ++b)
-        dst[b] = mac_word(c, s, b, bank);
-}
-
-// Writes the 112-byte preamble of source t (of nt) at dst (8-byte aligned):
-// the next source's plane loads (or no-ops), the wait for this source's
-// planes, the 22 composites, one s_nop.
-RJ_HD inline void emit_pre(uint64_t* dst, int t, int nt)
-{
-    uint32_t* w = reinterpret_cast<uint32_t*>(dst);
-    const int bank = t & 1, nb = (t + 1) & 1;
-    if (t + 1 < nt) {
-        const uint64_t a = enc_ds_read_b128(plane_reg(nb, 0), 20, (t + 1) * LDS_SRC);
-        const uint64_t b = enc_ds_read_b128(plane_reg(nb, 4), 20, (t + 1) * LDS_SRC + LDS_HALF);
-        w[0] = (uint32_t)a;
-        w[1] = (uint32_t)(a >> 32);
-        w[2] = (uint32_t)b;
-        w[3] = (uint32_t)(b >> 32);
-        w[4] = enc_waitcnt_lgkm(2);  // this source's two loads done, the next two in flight
-    } else {
-        w[0] = w[1] = w[2] = w[3] = S_NOP0;
-        w[4] = enc_waitcnt_lgkm(0);
+    uint8_t x = c, row[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int a = 0; a < 8; ++a) {  // row b bit a = bit b of c 2^a
+        for (int b = 0; b < 8; ++b)
+            row[b] |= (uint8_t)(((x >> b) & 1) << a);
+        x = (uint8_t)((x << 1) ^ ((x & 0x80) ? 0x1D : 0));
     }
-    int i = 5;
-    for (int hi = 0; hi < 2; ++hi)
-        for (int n = 1; n < 16; ++n) {
-            const int low = n & -n;
-#ifdef RSGPU_JIT_NCOMP
-            if (i >= 5 + RSGPU_JIT_NCOMP)
-                break;
-#endif
-            if (n != low)
-                w[i++] = enc_xor_e32(table_reg(bank, hi, n), table_reg(bank, hi, n ^ low),
-                                     table_reg(bank, hi, low));
-        }
-    while (i < PRE_BYTES / 4)
-        w[i++] = S_NOP0;  // 112 bytes
+    for (int b = 0; b < 8; ++b) {
+        const int acc = ACC + 8 * s + b, lo = row[b] & 15, hi = row[b] >> 4;
+        wd[b] = lo && hi ? enc_bitop3_96(acc, acc, table_reg(bank, 0, lo), table_reg(bank, 1, hi))
+                : lo     ? enc_xor_e64(acc, acc, table_reg(bank, 0, lo))
+                : hi     ? enc_xor_e64(acc, acc, table_reg(bank, 1, hi))
+                         : (uint64_t)S_NOP0 << 32 | S_NOP0;
+    }
 }
 
-// prologue (source 0's planes into bank A) at the chunk start
-RJ_HD inline void emit_prologue(uint64_t* dst)
+// 32-bit word i (< PRE_BYTES / 4 = 28) of source t's preamble: the next
+// source's two plane loads (or no-ops for the chunk's last source), the wait
+// for this source's planes, the 22 four-Russians composites, one s_nop
+RJ_HD inline uint32_t pre_u32(int t, int nt, int i)
 {
-    dst[0] = enc_ds_read_b128(plane_reg(0, 0), 20, 0);
-    dst[1] = enc_ds_read_b128(plane_reg(0, 4), 20, LDS_HALF);
+    const int bank = t & 1, nb = (t + 1) & 1;
+    if (i < 4) {
+        if (t + 1 >= nt)
+            return S_NOP0;
+        const uint64_t d = enc_ds_read_b128(plane_reg(nb, i < 2 ? 0 : 4), 20,
+                                            (t + 1) * LDS_SRC + (i < 2 ? 0 : LDS_HALF));
+        return (i & 1) ? (uint32_t)(d >> 32) : (uint32_t)d;
+    }
+    if (i == 4)
+        return enc_waitcnt_lgkm(t + 1 < nt ? 2 : 0);
+    const int j = i - 5;
+    if (j >= 22)
+        return S_NOP0;
+    // composites n = 3 5 6 7 9 10 11 12 13 14 15 of L, then of H
+    const int hi = j / 11, c = j - 11 * hi;
+    const int n = c < 1 ? 3 : c < 4 ? 4 + c : 5 + c;
+    const int low = n & -n;
+    return enc_xor_e32(table_reg(bank, hi, n), table_reg(bank, hi, n ^ low), table_reg(bank, hi, low));
 }
 
-RJ_HD inline void emit_epilogue(uint64_t* dst) { dst[0] = (uint64_t)S_NOP0 << 32 | S_SETPC_82; }
+// Word o (8 bytes) of chunk ch of a wave's code, for the wave's nslot rows
+// rows[s * k + q] (coefficient of row s, source q).  Returns false for words
+// past the chunk's return (never executed, not written).  k_jit_emit runs it
+// one word per thread; rsgpu_internal_jit_emit, for the CPU suite, too.
+RJ_HD inline bool code_word(const uint8_t* rows, int k, int nslot, int ch, int o, uint64_t* word)
+{
+    const int nt = k - 8 * ch < 8 ? k - 8 * ch : 8;
+    const int per_src = PRE_BYTES / 8 + 8 * nslot;
+    if (o < 2) {  // prologue: source 0's planes into bank A
+        *word = enc_ds_read_b128(plane_reg(0, 4 * o), 20, o * LDS_HALF);
+    } else if (o < 2 + nt * per_src) {
+        const int t = (o - 2) / per_src, r = o - 2 - t * per_src;
+        if (r < PRE_BYTES / 8) {
+            *word = (uint64_t)pre_u32(t, nt, 2 * r + 1) << 32 | pre_u32(t, nt, 2 * r);
+        } else {
+            const int m = r - PRE_BYTES / 8, s = m >> 3, pl = m & 7;
+            uint64_t wd[8];
+            mac_words(rows[s * k + 8 * ch + t], s, t & 1, wd);
+            *word = wd[pl];
+        }
+    } else if (o == 2 + nt * per_src) {
+        *word = (uint64_t)S_NOP0 << 32 | S_SETPC_82;
+    } else {
+        return false;
+    }
+    return true;
+}
 
 }  // namespace jit
 }  // namespace rsgpu

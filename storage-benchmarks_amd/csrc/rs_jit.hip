@@ -247,12 +247,15 @@ __global__ void k_jit_fill(uint64_t* code, long long n)
 
 }  // namespace jitk
 
-// One workgroup per (block, wave): the multiply-accumulate words one per
-// thread and iteration (coalesced), each source's preamble by one thread,
-// the chunks' ends last.  The wave's rows of the block's matrix are staged in
-// LDS first (a global load per word left the loop latency-bound), and one
-// workgroup per (block, wave, chunk) was dispatch-bound (0.49 ms for 32K
-// workgroups at C3).  Layout as rs_jit.h describes.
+// One workgroup per (block, wave), the wave's rows of the block's matrix
+// staged in LDS first: a thread per (source, slot) writes that coefficient's
+// eight multiply-accumulate words (one 64-byte run, consecutive threads
+// consecutive runs), a thread per preamble word, then the chunks' ends.
+// Layout as rs_jit.h describes; the words are those of jit::code_word (the
+// host emitter the CPU suite interprets).  (Earlier forms: emission inside
+// the prepare kernel, 0.41 ms at C3; one workgroup per (block, wave, chunk),
+// dispatch-bound at 0.49 ms; one thread per word with the index arithmetic
+// and the coefficient's matrix recomputed per word, 0.19 ms.)
 __global__ __launch_bounds__(256) void k_jit_emit(int k, int e, const uint8_t* coef, const int* status,
                                                   uint8_t* code)
 {
@@ -261,30 +264,39 @@ __global__ __launch_bounds__(256) void k_jit_emit(int k, int e, const uint8_t* c
     if (status[b] != 0)
         return;
     const int nw = (e + 7) / 8, nch = (k + 7) / 8;
-    const int nslot = min(8, e - 8 * w), per_src = nslot * 8;
+    const int nslot = min(8, e - 8 * w);
     const size_t stride = (size_t)jit::chunk_stride(8);
     uint8_t* cbase = code + ((size_t)b * nw + w) * nch * stride;
+    const int sb = jit::src_bytes(nslot);
     for (int i = threadIdx.x; i < nslot * k; i += blockDim.x)
         cw[i] = coef[((size_t)b * e + 8 * w) * k + i];
     __syncthreads();
-    for (int i = threadIdx.x; i < k * per_src; i += blockDim.x) {
-        const int q = i / per_src, r = i - q * per_src, s = r >> 3, pl = r & 7;
+    for (int i = threadIdx.x; i < 8 * k; i += blockDim.x) {
+        const int q = i >> 3, s = i & 7;
+        if (s >= nslot)
+            continue;
         const int ch = q >> 3, t = q & 7;
-        uint64_t* dst = reinterpret_cast<uint64_t*>(cbase + (size_t)ch * stride + jit::PRO_BYTES +
-                                                    (size_t)t * jit::src_bytes(nslot) + jit::PRE_BYTES);
-        dst[r] = jit::mac_word(cw[s * k + q], s, pl, t & 1);
+        uint64_t wd[8];
+        jit::mac_words(cw[s * k + q], s, t & 1, wd);
+        uint4* dst = reinterpret_cast<uint4*>(cbase + (size_t)ch * stride + jit::PRO_BYTES + (size_t)t * sb +
+                                              jit::PRE_BYTES + 64 * s);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            dst[j] = make_uint4((uint32_t)wd[2 * j], (uint32_t)(wd[2 * j] >> 32), (uint32_t)wd[2 * j + 1],
+                                (uint32_t)(wd[2 * j + 1] >> 32));
     }
-    for (int q = threadIdx.x; q < k; q += blockDim.x) {
-        const int ch = q >> 3, t = q & 7;
-        jit::emit_pre(reinterpret_cast<uint64_t*>(cbase + (size_t)ch * stride + jit::PRO_BYTES +
-                                                  (size_t)t * jit::src_bytes(nslot)),
-                      t, min(8, k - 8 * ch));
+    constexpr int PW = jit::PRE_BYTES / 8;  // preamble words per source
+    for (int i = threadIdx.x; i < PW * k; i += blockDim.x) {
+        const int q = i / PW, r = i - q * PW;
+        const int ch = q >> 3, t = q & 7, nt = min(8, k - 8 * ch);
+        reinterpret_cast<uint64_t*>(cbase + (size_t)ch * stride + jit::PRO_BYTES + (size_t)t * sb)[r] =
+            (uint64_t)jit::pre_u32(t, nt, 2 * r + 1) << 32 | jit::pre_u32(t, nt, 2 * r);
     }
-    for (int ch = threadIdx.x; ch < nch; ch += blockDim.x) {
-        uint8_t* base = cbase + (size_t)ch * stride;
-        jit::emit_prologue(reinterpret_cast<uint64_t*>(base));
-        jit::emit_epilogue(
-            reinterpret_cast<uint64_t*>(base + jit::PRO_BYTES + (size_t)min(8, k - 8 * ch) * jit::src_bytes(nslot)));
+    for (int i = threadIdx.x; i < 3 * nch; i += blockDim.x) {  // prologue words, return
+        const int ch = i / 3, o = i - 3 * ch, nt = min(8, k - 8 * ch);
+        uint64_t word;
+        (void)jit::code_word(cw, k, nslot, ch, o < 2 ? o : 2 + nt * (PW + 8 * nslot), &word);
+        reinterpret_cast<uint64_t*>(cbase + (size_t)ch * stride)[o < 2 ? o : 2 + nt * (PW + 8 * nslot)] = word;
     }
 }
 

@@ -1398,34 +1398,26 @@ long long rsgpu_internal_jit_matrix_code(int k, int e, const unsigned char* coef
 long long rsgpu_internal_jit_emit(int k, int e, const unsigned char* coef, unsigned char* out,
                                   size_t out_bytes)
 {
-    if (k <= 0 || e <= 0 || e > 32 || !coef)
+    if (k <= 0 || e <= 0 || k + e > 250 || !coef)
         return -1;
     const size_t need = jit_code_bytes(k, e, 1);
     if (!out || out_bytes < need)
         return (long long)need;
-    const int NW = (e + 7) / 8, nch = (k + 7) / 8;
-    const size_t stride = (size_t)jit::chunk_stride(8);
+    const int nw = (e + 7) / 8, nch = (k + 7) / 8, stride_w = jit::chunk_stride(8) / 8;
+    uint64_t* o64 = reinterpret_cast<uint64_t*>(out);
     for (size_t i = 0; i < need / 8; ++i)
-        reinterpret_cast<uint64_t*>(out)[i] = (uint64_t)jit::S_NOP0 << 32 | jit::S_SETPC_82;
-    for (int w = 0; w < NW; ++w)
-        for (int q = 0; q < k; ++q) {
-            const int ch = q / 8, t = q - 8 * ch, ntc = std::min(8, k - 8 * ch);
-            const int nslot = std::min(8, e - 8 * w);
-            uint64_t* dst = reinterpret_cast<uint64_t*>(out + ((size_t)w * nch + ch) * stride +
-                                                        jit::PRO_BYTES + (size_t)t * jit::src_bytes(nslot));
-            jit::emit_pre(dst, t, ntc);
-            for (int s = 0; s < nslot; ++s)
-                jit::emit_mac(dst + jit::PRE_BYTES / 8 + 8 * s, coef[(size_t)(8 * w + s) * k + q], s,
-                              t & 1);
-        }
-    for (int w = 0; w < NW; ++w)
-        for (int ch = 0; ch < nch; ++ch) {
-            const int ntc = std::min(8, k - 8 * ch), nslot = std::min(8, e - 8 * w);
-            unsigned char* base = out + ((size_t)w * nch + ch) * stride;
-            jit::emit_prologue(reinterpret_cast<uint64_t*>(base));
-            jit::emit_epilogue(reinterpret_cast<uint64_t*>(base + jit::PRO_BYTES +
-                                                           (size_t)ntc * jit::src_bytes(nslot)));
-        }
+        o64[i] = (uint64_t)jit::S_NOP0 << 32 | jit::S_SETPC_82;
+    // the words k_jit_emit writes, from the same function
+    for (int w = 0; w < nw; ++w) {
+        const int nslot = std::min(8, e - 8 * w);
+        const unsigned char* rows = coef + (size_t)8 * w * k;
+        for (int ch = 0; ch < nch; ++ch)
+            for (int o = 0; o < stride_w; ++o) {
+                uint64_t word;
+                if (jit::code_word(rows, k, nslot, ch, o, &word))
+                    o64[((size_t)w * nch + ch) * stride_w + o] = word;
+            }
+    }
     return (long long)need;
 }
 

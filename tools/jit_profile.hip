@@ -95,25 +95,19 @@ int main(int argc, char** argv)
         uint8_t* cb = (uint8_t*)code.data() + (size_t)b * per;
         for (size_t i = 0; i < per / 8; ++i)
             ((uint64_t*)cb)[i] = (uint64_t)jit::S_NOP0 << 32 | jit::S_SETPC_82;
+        std::vector<uint8_t> rows((size_t)e * k);
+        for (auto& c : rows) {
+            x = x * 1664525u + 1013904223u;
+            c = (uint8_t)(x >> 13);
+        }
+        const int stride_w = (int)(stride / 8);
         for (int w = 0; w < NW; ++w)
-            for (int q = 0; q < k; ++q) {
-                const int ch = q / 8, t = q - 8 * ch, ntc = std::min(8, k - 8 * ch);
-                const int nslot = std::min(8, e - 8 * w);
-                uint64_t* dst = (uint64_t*)(cb + ((size_t)w * nch + ch) * stride + jit::PRO_BYTES +
-                                            (size_t)t * jit::src_bytes(nslot));
-                jit::emit_pre(dst, t, ntc);
-                for (int s = 0; s < nslot; ++s) {
-                    x = x * 1664525u + 1013904223u;
-                    jit::emit_mac(dst + jit::PRE_BYTES / 8 + 8 * s, (uint8_t)(x >> 13), s, t & 1);
+            for (int ch = 0; ch < nch; ++ch)
+                for (int o = 0; o < stride_w; ++o) {
+                    uint64_t word;
+                    if (jit::code_word(rows.data() + (size_t)8 * w * k, k, std::min(8, e - 8 * w), ch, o, &word))
+                        ((uint64_t*)cb)[((size_t)w * nch + ch) * stride_w + o] = word;
                 }
-            }
-        for (int w = 0; w < NW; ++w)
-            for (int ch = 0; ch < nch; ++ch) {
-                const int ntc = std::min(8, k - 8 * ch), nslot = std::min(8, e - 8 * w);
-                uint8_t* base = cb + ((size_t)w * nch + ch) * stride;
-                jit::emit_prologue((uint64_t*)base);
-                jit::emit_epilogue((uint64_t*)(base + jit::PRO_BYTES + (size_t)ntc * jit::src_bytes(nslot)));
-            }
     }
     uint64_t* d_stage;
     (void)hipMalloc(&d_stage, code.size() * 8);
