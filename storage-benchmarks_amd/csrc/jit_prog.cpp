@@ -46,7 +46,7 @@ void full_tables(const uint8_t (&masks)[64], int nm, SrcProg& p)
 
 }  // namespace
 
-void plan_source(const uint8_t* coef, int nslot, SrcProg& p)
+void plan_source(const uint8_t* coef, int nslot, SrcProg& p, int max_ops)
 {
     uint8_t masks[64];
     const int nm = 8 * nslot;
@@ -86,7 +86,7 @@ void plan_source(const uint8_t* coef, int nslot, SrcProg& p)
                 nl[nneed++] = (uint8_t)m;
         if (!nneed)
             break;
-        if (p.nops == kMaxComposites) {
+        if (p.nops == max_ops || p.nops == kMaxComposites) {
             over = true;
             break;
         }
@@ -218,7 +218,7 @@ size_t emit_chunk(uint8_t* dst, int nt, int nslot, const SrcProg* progs)
     return o;
 }
 
-std::vector<uint8_t> build_matrix_code(const uint8_t* c, int k, int e, int* chunk_stride)
+std::vector<uint8_t> build_matrix_code(const uint8_t* c, int k, int e, int* chunk_stride, int max_ops)
 {
     const int stride = host_chunk_stride(), nch = (k + 7) / 8, passes = (e + 31) / 32;
     *chunk_stride = stride;
@@ -239,7 +239,7 @@ std::vector<uint8_t> build_matrix_code(const uint8_t* c, int k, int e, int* chun
                     uint8_t cf[8];
                     for (int s = 0; s < nslot; ++s)
                         cf[s] = c[(size_t)(32 * p + 8 * w + s) * k + 8 * ch + t];
-                    plan_source(cf, nslot, progs[t]);
+                    plan_source(cf, nslot, progs[t], max_ops);
                 }
                 emit_chunk(&code[(((size_t)p * 4 + w) * nch + ch) * stride], nt, nslot, progs);
             }

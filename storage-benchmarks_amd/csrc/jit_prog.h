@@ -36,7 +36,7 @@ struct SrcProg {
 
 // Cover of the masks of coefficients coef[0..nslot-1] (slot s = output row
 // 8 w + s of the wave).
-void plan_source(const uint8_t* coef, int nslot, SrcProg& p);
+void plan_source(const uint8_t* coef, int nslot, SrcProg& p, int max_ops = kMaxComposites);
 
 // Largest chunk (8 sources, 8 slots, kMaxComposites 3-input composites),
 // rounded to 64-byte lines: the stride between chunks of host-built code.
@@ -49,7 +49,10 @@ size_t emit_chunk(uint8_t* dst, int nt, int nslot, const SrcProg* progs);
 // The whole program of an e x k matrix c (row-major) in passes of <= 32
 // rows: pass p, wave w, chunk ch at ((p NW_MAX + w) nch + ch) stride, with
 // NW_MAX = 4 wave slots reserved per pass.  Returns the bytes.
-std::vector<uint8_t> build_matrix_code(const uint8_t* c, int k, int e, int* chunk_stride);
+// max_ops < kMaxComposites caps the greedy cover (tests use it to exercise
+// the full-table fallback).
+std::vector<uint8_t> build_matrix_code(const uint8_t* c, int k, int e, int* chunk_stride,
+                                       int max_ops = kMaxComposites);
 
 }  // namespace jit
 }  // namespace rsgpu

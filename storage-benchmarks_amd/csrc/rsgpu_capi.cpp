@@ -1380,11 +1380,11 @@ int rsgpu_fill_synthetic(rsgpu_ctx* ctx, unsigned char* d_rows, size_t rows, siz
 // suite to disassemble and interpret.  Returns the bytes needed, or -1;
 // writes only when out_bytes is large enough; *chunk_stride gets the stride.
 long long rsgpu_internal_jit_matrix_code(int k, int e, const unsigned char* coef, unsigned char* out,
-                                         size_t out_bytes, int* chunk_stride)
+                                         size_t out_bytes, int* chunk_stride, int max_ops)
 {
     if (k <= 0 || k > 250 || e <= 0 || e > 255 || !coef || !chunk_stride)
         return -1;
-    const std::vector<uint8_t> code = jit::build_matrix_code(coef, k, e, chunk_stride);
+    const std::vector<uint8_t> code = jit::build_matrix_code(coef, k, e, chunk_stride, max_ops);
     if (out && out_bytes >= code.size())
         std::memcpy(out, code.data(), code.size());
     return (long long)code.size();
