@@ -1,13 +1,14 @@
-// rs_jit.h -- per-block generated decode code (k_rs_jit, rs_jit.hip).
+// rs_jit.h -- generated decode / encode code (k_rs_jit, rs_jit.hip).
 //
 // The one-matrix decode applies an e x k coefficient matrix that differs per
 // block (random erasures).  k_rs_tc dispatches each coefficient through a
-// handler (a jump, SALU work and GPR-index mode per coefficient); here the
-// prepare kernel instead WRITES the straight-line code of every (block,
-// wave, chunk of 8 sources) into executable device memory, with the
-// coefficients baked into the register operands, and the decode kernel
-// makes one call per chunk.  Only vector-ALU, LDS-read, s_waitcnt, s_nop
-// and s_setpc instructions are ever generated.
+// handler (a jump, SALU work and GPR-index mode per coefficient); here
+// k_jit_emit instead WRITES the straight-line code of every (block, wave,
+// chunk of 8 sources) into executable device memory, with the coefficients
+// baked into the register operands, and the decode kernel makes one call per
+// chunk.  The encode of a matrix shared by every block gets the same kind of
+// code, built once on the host (jit_prog.h).  Only vector-ALU, LDS-read,
+// s_waitcnt, s_nop and s_setpc instructions are ever generated.
 //
 // Register contract (the decode kernel's asm statement clobbers all of it):
 //   v20            LDS byte address of the chunk's first source + 16 lane
@@ -29,7 +30,8 @@
 //              multiply-accumulates of 8 bytes each (v_bitop3_b32 0x96 /
 //              v_xor_b32_e64 / s_nop pair for a zero row)       112 + 64 nslot B
 //   epilogue   s_setpc_b64 s[82:83]; s_nop                           8 B
-// The layout depends on (nt, nslot) only, never on the coefficients.
+// The layout depends on (nt, nslot) only, never on the coefficients (the
+// host-built shared programs of jit_prog.h size each preamble to its cover).
 #pragma once
 #include <stdint.h>
 
