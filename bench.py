@@ -81,6 +81,9 @@ def parse(argv=None):
     p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r02_traffic.json"),
                    help="JSON with PMC-derived HBM bytes per launch of the same workload "
                         "(tools/profile_round.sh)")
+    p.add_argument("--sq-counters", default=os.path.join(ROOT, "profiles", "r02_sq_counters.txt"),
+                   help="SQ counter summary of the same workload (tools/pmc_sq.sh + "
+                        "tools/pmc_summary.py): VALU-issue roofline of each kernel")
     # testing the N-rank path on a one-GPU box: every rank on device 0, gloo
     # for the barrier / max-time reduction (RCCL needs one GPU per rank)
     p.add_argument("--same-device", action="store_true", help=argparse.SUPPRESS)
@@ -406,6 +409,40 @@ def kernel_stats(recs, steps, alg):
     return per, kernels
 
 
+# SIMD cycles per wave64 v_bitop3 / v_xor with >= 4 waves per SIMD
+# (tools/ubench_bank.hip, profiles/r02_ubench_bank.log): the VALU issue limit
+VALU_CYCLES_PER_INST = 2.6
+SIMDS = 1024  # 256 CUs x 4
+
+
+def sq_counters(path):
+    """{kernel: {counter: value per dispatch}} from tools/pmc_summary.py output."""
+    out, cur = {}, None
+    for ln in open(path):
+        if not ln.startswith(" "):
+            cur = ln.strip()
+            out[cur] = {}
+        elif cur is not None:
+            name, val = ln.split()
+            out[cur][name] = float(val)
+    return out
+
+
+def valu_roofline(counters, kernel, avg_ms):
+    """VALU-issue roofline of one kernel launch: the time its VALU
+    instructions need at the issue limit, at the clock the launch ran at
+    (GRBM_GUI_ACTIVE over 8 XCDs), against its measured time."""
+    c = counters.get(kernel) or counters.get(kernel.split("(")[0])
+    if not c or "SQ_INSTS_VALU" not in c or "GRBM_GUI_ACTIVE" not in c:
+        return None
+    ghz = c["GRBM_GUI_ACTIVE"] / 8 / (avg_ms * 1e-3) / 1e9
+    need_ms = c["SQ_INSTS_VALU"] * VALU_CYCLES_PER_INST / SIMDS / (ghz * 1e9) * 1e3
+    return {"valu_insts_per_launch": c["SQ_INSTS_VALU"],
+            "valu_insts_per_wave": round(c["SQ_INSTS_VALU"] / c["SQ_WAVES"], 1) if c.get("SQ_WAVES") else None,
+            "clock_ghz": round(ghz, 3), "cycles_per_inst": VALU_CYCLES_PER_INST,
+            "issue_bound_ms": round(need_ms, 3), "frac": round(need_ms / avg_ms, 4)}
+
+
 def alg_bytes(k, e, L):
     """Algorithmic HBM bytes per BLOCK of each kernel:
     (k + e) L for an encode or a decode (read k rows, write e)."""
@@ -645,6 +682,11 @@ def main(argv=None):
             and not custom):
         traffic = json.load(open(args.traffic)).get(dom)
         traffic_src = os.path.relpath(args.traffic, ROOT) if traffic is not None else None
+    valu = None
+    if (args.sq_counters and os.path.exists(args.sq_counters) and args.config == "c3"
+            and not args.blocks and not custom):
+        sq = sq_counters(args.sq_counters)
+        valu = {kn: r for kn in per if (r := valu_roofline(sq, kn, per[kn][0] / per[kn][1]))}
     op_bytes = float((k + e) * L) * (out_bytes_step / (2.0 * e * L))
     step_frac = (2 * op_bytes) / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBPS
 
@@ -668,7 +710,11 @@ def main(argv=None):
                      "alg_bytes_per_launch": dom_bytes, "avg_ms": round(dom_ms, 3),
                      # north_star's HBM-read variant: only the k source rows read
                      # per block count
-                     "frac_read": round(read_bytes / (dom_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)},
+                     "frac_read": round(read_bytes / (dom_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+                     # what bounds the kernels instead: VALU issue at the
+                     # power-limited clock (SQ counters of the same workload)
+                     "valu": valu,
+                     "valu_source": (os.path.relpath(args.sq_counters, ROOT) if valu else None)},
         "cpu_baseline": None,
     }
     line.update(extra)
