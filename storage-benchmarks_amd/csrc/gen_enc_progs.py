@@ -17,6 +17,13 @@ Also the Horner twiddles (row r times 2^(C r) between chunks) as XOR
 programs over the row's 8 accumulator planes: TwProg<K, E, C, R> with NOPS,
 ops (as below) and outs[8] = the value that becomes plane b.
 
+Source T = 0 of every chunk has the coefficient 2^0 = 1 on every row, so
+each of its outputs is a single plane.  T0Pair<K, E, C, R0, NR>::partner[o]
+names the first later source of the chunk whose output o is a single value
+too; that source adds both terms with one 3-input XOR (acc ^= V[x] ^ p0[b])
+and source 0 skips output o (0 = no partner: source 0 adds its plane).  On
+the (64, 32) plan 204 of the 256 source-0 outputs per chunk find a partner.
+
 Output: C++ specializations EncProg<K, E, C, R0, NR, T> with
   NOPS, ops[NOPS][3]  value 8 + i = XOR of values ops[i][0..2] (255 = none)
   outs[NR * 8][2]     acc[s][b] ^= values outs[s*8+b][0] ^ outs[s*8+b][1]
@@ -31,6 +38,9 @@ import sys
 PLANS = [(16, 4, 16, 1), (16, 8, 16, 1), (64, 32, 16, 4), (64, 16, 16, 2), (100, 20, 20, 4),
          (5, 4, 5, 1), (20, 7, 20, 1)]
 NONE = 255
+# plans whose kernel would spill with source 0's planes held across the chunk
+# (k_rs_bs<100, 20>: 128 VGPRs + 2 spilled, 122 without pairing)
+NO_T0_PAIR = {(100, 20, 20)}
 
 
 def gf_mul(a: int, b: int) -> int:
@@ -165,6 +175,20 @@ def block(K, E, C, R0, NR, T):
     return ops, vals, outs
 
 
+def t0_partners(K, E, C, R0, NR):
+    """partner[o] for T0Pair (see the module docstring); all zeros when a
+    chunk may be partial (K % C != 0)."""
+    part = [0] * (NR * 8)
+    if K % C or (K, E, C) in NO_T0_PAIR:
+        return part
+    for T in range(1, C):
+        _, _, outs = block(K, E, C, R0, NR, T)
+        for o, (x, y) in enumerate(outs):
+            if part[o] == 0 and x != NONE and y == NONE:
+                part[o] = T
+    return part
+
+
 def main():
     out = ["// generated by gen_enc_progs.py -- do not edit"]
     total = nblk = 0
@@ -186,6 +210,10 @@ def main():
                 out.append(f"    static constexpr uint8_t ops[{max(1, len(ops))}][3] = {{{o}}};")
                 out.append(f"    static constexpr uint8_t outs[{NR * 8}][2] = {{{w}}};")
                 out.append("};")
+            part = t0_partners(K, E, C, R0, NR)
+            out.append(f"template <> struct T0Pair<{K}, {E}, {C}, {R0}, {NR}> {{")
+            out.append(f"    static constexpr uint8_t partner[{NR * 8}] = {{{', '.join(map(str, part))}}};")
+            out.append("};")
     out.append(f"// {nblk} blocks, {total / max(1, nblk):.2f} composite XORs per source on average")
     # Horner twiddles: row r of a plan with chunk C is multiplied by 2^(C r)
     tw_total = tw_n = 0

@@ -20,7 +20,10 @@
 //     p_r = sum_c 2^(C r c) * E_c(r),   E_c(r) = sum_t 2^(r t) d_{cC+t},
 // so one chunk's straight-line code (coefficients 2^(r t), t < C) serves
 // every chunk; between chunks each accumulator is multiplied by the constant
-// 2^(C r) (~16 XORs).  The chunk loop is a runtime loop.
+// 2^(C r) (~16 XORs).  The chunk loop is a runtime loop.  A chunk's source 0
+// has the coefficient 1 on every row: its single-plane terms ride along in
+// the 3-input XOR of a later source whose term is a single value too
+// (T0Pair, gen_enc_progs.py), 3 % fewer instructions at (64, 32).
 //
 // Work split: a workgroup of NW waves shares 64 x 32 = 2048 byte positions;
 // wave w owns outputs [w*OPW, (w+1)*OPW) (8 planes x OPW accumulators in
@@ -55,6 +58,8 @@ template <int K, int E, int C, int R0, int NR, int T>
 struct EncProg;
 template <int K, int E, int C, int R>
 struct TwProg;
+template <int K, int E, int C, int R0, int NR>
+struct T0Pair;
 #include "enc_progs.inc"
 
 template <class PR, int I, int NV>
@@ -92,22 +97,33 @@ __device__ __forceinline__ void prog_op(uint32_t (&V)[NV])
         V[8 + I] = x3(V[a], V[b], V[c]);
 }
 
-template <class PR, int O, int NV>
-__device__ __forceinline__ void prog_out(uint32_t& acc, const uint32_t (&V)[NV])
+// Output O of source T: its one or two values; source 0's single plane
+// moves to the partner source of T0Pair (one 3-input XOR for both terms)
+template <class PR, class PP, int T, int O, int NV>
+__device__ __forceinline__ void prog_out(uint32_t& acc, const uint32_t (&V)[NV], const uint32_t (&p0)[8])
 {
     constexpr int x = PR::outs[O][0], y = PR::outs[O][1];
-    if constexpr (x != 255 && y != 255)
+    constexpr int partner = PP::partner[O];
+    if constexpr (T == 0 && partner != 0) {
+        // added by source `partner`
+    } else if constexpr (T != 0 && partner == T) {
+        static_assert(x != 255 && y == 255, "T0 partner output must be a single value");
+        acc = x3(acc, V[x], p0[O % 8]);
+    } else if constexpr (x != 255 && y != 255) {
         acc = x3(acc, V[x], V[y]);
-    else if constexpr (x != 255)
+    } else if constexpr (x != 255) {
         acc ^= V[x];
+    }
 }
 
 // consume source T of the chunk from planes p (all lanes), for this wave's
 // rows: the generated program's composites, then one XOR per output plane
+// (p0: the chunk's source 0 planes, for the outputs paired with it)
 template <class P, int R0, int NR, int T>
-__device__ __forceinline__ void consume(uint32_t (&acc)[NR][8], const uint32_t (&p)[8])
+__device__ __forceinline__ void consume(uint32_t (&acc)[NR][8], const uint32_t (&p)[8], const uint32_t (&p0)[8])
 {
     using PR = EncProg<P::k, P::e, P::c, R0, NR, T>;
+    using PP = T0Pair<P::k, P::e, P::c, R0, NR>;
     constexpr int NV = 8 + PR::NOPS;
     uint32_t V[NV];
 #pragma unroll
@@ -117,7 +133,7 @@ __device__ __forceinline__ void consume(uint32_t (&acc)[NR][8], const uint32_t (
         (prog_op<PR, Is>(V), ...);
     }(std::make_integer_sequence<int, PR::NOPS>{});
     [&]<int... Os>(std::integer_sequence<int, Os...>) {
-        (prog_out<PR, Os>(acc[Os / 8][Os % 8], V), ...);
+        (prog_out<PR, PP, T, Os>(acc[Os / 8][Os % 8], V, p0), ...);
     }(std::make_integer_sequence<int, NR * 8>{});
 }
 
@@ -134,8 +150,8 @@ constexpr int S = 8;
 
 // Sources T = PART*S + t (t < S, T < C) of the current chunk from the LDS part.
 template <class P, int K, int C, int R0, int NR, int PART>
-__device__ __forceinline__ void consume_part(uint32_t (&acc)[NR][8], const uint4* buf, int lane,
-                                             int j0)
+__device__ __forceinline__ void consume_part(uint32_t (&acc)[NR][8], uint32_t (&p0)[8], const uint4* buf,
+                                             int lane, int j0)
 {
     [&]<int... Ts>(std::integer_sequence<int, Ts...>) {
         (
@@ -146,7 +162,12 @@ __device__ __forceinline__ void consume_part(uint32_t (&acc)[NR][8], const uint4
                         const uint4 u = buf[(Ts * 2 + 0) * 64 + lane];
                         const uint4 v = buf[(Ts * 2 + 1) * 64 + lane];
                         const uint32_t pl[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
-                        consume<P, R0, NR, T>(acc, pl);
+                        if constexpr (T == 0) {
+#pragma unroll
+                            for (int a = 0; a < 8; ++a)
+                                p0[a] = pl[a];
+                        }
+                        consume<P, R0, NR, T>(acc, pl, p0);
                     }
                     // keep the next source's LDS reads from being hoisted
                     // here (they would pin 8 more VGPRs per source)
@@ -207,6 +228,7 @@ __device__ __forceinline__ void run_group(const Args& a, uint4 (*lds)[S * 2 * 64
     };
 
     uint32_t acc[NR][8];
+    uint32_t p0[8] = {};  // planes of the current chunk's source 0 (T0Pair)
 #pragma unroll
     for (int r = 0; r < NR; ++r)
 #pragma unroll
@@ -238,7 +260,7 @@ __device__ __forceinline__ void run_group(const Args& a, uint4 (*lds)[S * 2 * 64
             twiddle_rows<P, R0, NR>(acc, std::make_integer_sequence<int, NR>{});
         // consume part `part` of the chunk: compile-time T = part*S + t
         [&]<int... Ps>(std::integer_sequence<int, Ps...>) {
-            ((part == Ps ? consume_part<P, K, C, R0, NR, Ps>(acc, buf, lane, j0)
+            ((part == Ps ? consume_part<P, K, C, R0, NR, Ps>(acc, p0, buf, lane, j0)
                          : void()),
              ...);
         }(std::make_integer_sequence<int, NP>{});

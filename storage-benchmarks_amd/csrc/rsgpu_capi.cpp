@@ -965,6 +965,11 @@ enum class Plan {
 // code; below kJitXcdTiles the decode runs in XCD-contiguous order
 constexpr size_t kJitMinTiles = 48;
 constexpr size_t kJitXcdTiles = 128;
+// (block, tile) pairs per call from which AUTO pays the emission launch
+// (~10 us whatever the batch) for the ~4 ns per pair the generated code saves
+// over threaded code: C2 (one block, 489 tiles) decodes 16 us threaded
+// against 10 + 11 us emitted + generated (profiles/r02_ab/c2_*.json)
+constexpr size_t kJitMinWork = 4096;
 
 bool rows_aligned(size_t len, size_t pitch, const void* a, const void* b, const void* c)
 {
@@ -982,7 +987,7 @@ Plan general_plan(rsgpu_ctx* ctx, size_t len)
     return Plan::general_tc;
 }
 
-Plan decode_plan(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch, const void* src,
+Plan decode_plan(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch, size_t blocks, const void* src,
                  const void* par, const void* out)
 {
     if (!rows_aligned(len, pitch, src, par, out) || !tc_ready(ctx))
@@ -1006,7 +1011,8 @@ Plan decode_plan(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch, const v
     // it): C3 / C5 (489 tiles) 25.2 / 15.0 ms vs 27 / 17.7 threaded; L =
     // 128000 (63 tiles) 3.79 vs 3.94 ms; C4 (16 tiles) 14.7 + 1.25 emission
     // vs 15.0 per 16384 blocks (profiles/r02_ab)
-    if (want == RSGPU_DECODE_AUTO && (len + 2047) / 2048 < kJitMinTiles)
+    if (want == RSGPU_DECODE_AUTO &&
+        ((len + 2047) / 2048 < kJitMinTiles || (len + 2047) / 2048 * blocks < kJitMinWork))
         return Plan::one_matrix;
     return Plan::generated;
 }
@@ -1179,7 +1185,7 @@ int rsgpu_decode_prepare(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch,
     if (blocks > kMaxGridBlocks)
         return fail(ctx, RSGPU_ERR_ARG, "rsgpu_decode_prepare: at most 65535 blocks per call "
                                         "(rsgpu_decode_blocks slices larger batches)");
-    const Plan plan = decode_plan(ctx, k, e, len, pitch, d_src, d_parity, d_out);
+    const Plan plan = decode_plan(ctx, k, e, len, pitch, blocks, d_src, d_parity, d_out);
     if (plan == Plan::one_matrix || plan == Plan::fused || plan == Plan::generated) {
         const WsLayout w = ws_layout(k, e, blocks);
         char* ws = (char*)d_workspace;
@@ -1226,7 +1232,7 @@ int rsgpu_decode_apply(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch, s
     if (blocks > kMaxGridBlocks)
         return fail(ctx, RSGPU_ERR_ARG, "rsgpu_decode_apply: at most 65535 blocks per call "
                                         "(rsgpu_decode_blocks slices larger batches)");
-    const Plan plan = decode_plan(ctx, k, e, len, pitch, d_src, d_parity, d_out);
+    const Plan plan = decode_plan(ctx, k, e, len, pitch, blocks, d_src, d_parity, d_out);
     const WsLayout w = ws_layout(k, e, blocks);
     char* ws = (char*)d_workspace;
     if (plan == Plan::generated)

@@ -240,3 +240,43 @@ def test_twiddle_programs():
                 assert V[outs[b]] == ge.mat_row(c, b), (K, E, C, r, b)
             n += 1
     assert n == sum(E for _, E, _, _ in ge.PLANS)
+
+
+def test_encode_t0_pairing_chunk():
+    """k_rs_bs with T0Pair (gen_enc_progs.py): a chunk's source 0 (coefficient
+    1 on every row) adds no term of its own to an output that a later source
+    adds together with its single value; over a whole chunk every output plane
+    still equals sum_T 2^(r T) d_T, evaluated symbolically over the 8 C
+    source planes of the chunk (bit 8 T + a = plane a of source T)."""
+    npair = 0
+    for K, E, C, NW in ge.PLANS:
+        opw = (E + NW - 1) // NW
+        for grp in range(NW):
+            R0, NR = grp * opw, min(opw, E - grp * opw)
+            part = ge.t0_partners(K, E, C, R0, NR)
+            acc = [0] * (NR * 8)
+            for T in range(C):
+                ops, vals, outs = ge.block(K, E, C, R0, NR, T)
+                V = [1 << (8 * T + a) for a in range(8)]
+                for op in ops:
+                    x = 0
+                    for i in op:
+                        if i != ge.NONE:
+                            x ^= V[i]
+                    V.append(x)
+                for o, (x, y) in enumerate(outs):
+                    if T == 0 and part[o]:
+                        continue
+                    if T and part[o] == T:
+                        assert x != ge.NONE and y == ge.NONE
+                        acc[o] ^= V[x] ^ (1 << (o % 8))  # source 0's plane b
+                        npair += 1
+                        continue
+                    acc[o] ^= (V[x] if x != ge.NONE else 0) ^ (V[y] if y != ge.NONE else 0)
+            for o in range(NR * 8):
+                r, b = R0 + o // 8, o % 8
+                exp = 0
+                for T in range(C):
+                    exp |= ge.mat_row(ge.gf_pow2(r * T), b) << (8 * T)
+                assert acc[o] == exp, (K, E, C, R0, o)
+    assert npair > 0

@@ -425,3 +425,23 @@ def test_batch_beyond_grid_limit(ctx, orc, kernel):
             assert all((got[i] == rec[i]).all() for i in range(e)), b
     finally:
         ctx.set_decode_kernel("auto")
+
+
+@pytest.mark.parametrize("blocks,name", [(1, "k_rs_tc(decode)"), (9, "k_rs_jit(decode)")])
+def test_auto_decode_kernel_by_batch_work(ctx, blocks, name):
+    """AUTO decodes a batch with fewer than 4096 (block, 2 KB tile) pairs
+    through threaded code (the generated code's emission launch is not paid
+    back: C2, one full-row block) and larger batches through generated code;
+    both with the erased rows poisoned, recovered bytes intact."""
+    k, e, L = 16, 4, 1000000
+    ctx.set_decode_kernel("auto")
+    enc = rsgpu.GpuEncoder(k, L, e, blocks=blocks, seed=29, ctx=ctx)
+    enc.encode_all()
+    dec = rsgpu.GpuDecoder(k, L, e, blocks=blocks, seed=29, ctx=ctx)
+    ctx.timing_read()
+    ctx.timing_enable(True)
+    ok = decode_poisoned(ctx, enc, dec)
+    names = [n for n, _, _ in ctx.timing_read()]
+    ctx.timing_enable(False)
+    assert ok
+    assert name in names and names[-1] == name, names
