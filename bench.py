@@ -36,6 +36,7 @@ import math
 import os
 import shutil
 import socket
+import statistics
 import subprocess
 import sys
 import time
@@ -394,15 +395,17 @@ def cpu_baseline(k, e, L, threads, kernel=1, blocks_per_thread=None, one_thread_
 
 
 def kernel_stats(recs, steps, alg):
-    per = {}
+    per, each = {}, {}
     for name, ms, nb in recs:
         d = per.setdefault(name, [0.0, 0, 0])
         d[0] += ms
         d[1] += 1
         d[2] += nb
+        each.setdefault(name, []).append(ms)
     kernels = {}
     for name, (tot, n, nb) in per.items():
-        kernels[name] = {"avg_ms": round(tot / n, 3), "launches": n,
+        kernels[name] = {"avg_ms": round(tot / n, 3), "median_ms": round(statistics.median(each[name]), 3),
+                         "launches": n,
                          "blocks_per_launch": nb / n,
                          "alg_GBps": round(alg.get(name, 0.0) * nb / (tot * 1e-3) / 1e9, 1),
                          "ms_per_step": round(tot / steps, 3)}
