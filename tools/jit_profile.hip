@@ -59,6 +59,10 @@ int main(int argc, char** argv)
     const int e = argc > 3 ? atoi(argv[3]) : 32;
     // extra dynamic LDS per workgroup: caps workgroups per CU (occupancy A/B)
     const int extra_lds = argc > 4 ? atoi(argv[4]) : 0;
+    // order of the independent multiply-accumulate words of a source (A/B of
+    // operand locality): 0 = as emitted (slot, plane), 1 = by (L, H) operand
+    // registers, 2 = by (H, L)
+    const int mac_order = argc > 5 ? atoi(argv[5]) : 0;
     const long long L = 1000000, pitch = 1000192;
     uint8_t* rows;
     if (hipMalloc(&rows, (size_t)B * (k + e) * pitch) != hipSuccess) {
@@ -103,10 +107,25 @@ int main(int argc, char** argv)
         const int stride_w = (int)(stride / 8);
         for (int w = 0; w < NW; ++w)
             for (int ch = 0; ch < nch; ++ch)
+            {
                 for (int o = 0; o < stride_w; ++o) {
                     uint64_t word;
                     if (jit::code_word(rows.data() + (size_t)8 * w * k, k, std::min(8, e - 8 * w), ch, o, &word))
                         ((uint64_t*)cb)[((size_t)w * nch + ch) * stride_w + o] = word;
+                }
+                    if (mac_order) {
+                        const int nt = std::min(8, k - 8 * ch), nslot = std::min(8, e - 8 * w);
+                        for (int t = 0; t < nt; ++t) {
+                            uint64_t* m = (uint64_t*)(cb + ((size_t)w * nch + ch) * stride + jit::PRO_BYTES +
+                                                      (size_t)t * jit::src_bytes(nslot) + jit::PRE_BYTES);
+                            auto key = [&](uint64_t wd) {
+                                const uint32_t w1 = (uint32_t)(wd >> 32);
+                                const uint32_t L = (w1 >> 9) & 511, H = (w1 >> 18) & 511;
+                                return mac_order == 1 ? (L << 9 | H) : (H << 9 | L);
+                            };
+                            std::stable_sort(m, m + 8 * nslot, [&](uint64_t x, uint64_t y) { return key(x) < key(y); });
+                        }
+                    }
                 }
     }
     uint64_t* d_stage;
