@@ -57,7 +57,10 @@ def encode_and_check(ctx, orc, k, e, L, B, coef=None, seed=5):
 @pytest.mark.parametrize("kernel", KERNELS)
 @pytest.mark.parametrize("k,e,L,B", [(64, 32, 65536, 3), (16, 4, 32000, 2), (100, 20, 8192, 2),
                                      (32, 16, 4096, 5), (128, 64, 2048, 2), (9, 40, 1024, 2),
-                                     (20, 13, 96, 3), (250 - 37, 37, 64, 2)], ids=str)
+                                     (20, 13, 96, 3), (250 - 37, 37, 64, 2),
+                                     # the other compiled codes (k_rs_bs, source 0 pairing)
+                                     (16, 8, 8192, 2), (64, 16, 4096, 2), (5, 4, 2048, 3), (20, 7, 4096, 2)],
+                         ids=str)
 def test_encode_kernels_rs(ctx, orc, kernel, k, e, L, B):
     ctx.set_encode_kernel(kernel)
     try:
