@@ -192,7 +192,10 @@ int rsgpu_decode_blocks(rsgpu_ctx *ctx, int k, int e, size_t len, size_t pitch, 
  * prepare followed by apply on the same stream.  apply may fan work out to an
  * internal second stream; it always joins back, so everything it wrote is
  * ordered before later work on the context stream.  At most 65535 blocks
- * per call (RSGPU_ERR_ARG beyond). */
+ * per call (RSGPU_ERR_ARG beyond).  apply must be given the geometry, block
+ * count, buffers and workspace of the prepare before it, with no
+ * rsgpu_set_decode_kernel in between: both derive the decode kernel (and so
+ * the workspace layout) from them. */
 int rsgpu_decode_prepare(rsgpu_ctx *ctx, int k, int e, size_t len, size_t pitch, size_t blocks,
                          const unsigned char *d_src, const unsigned char *d_parity,
                          const unsigned char *d_err, unsigned char *d_out, void *d_workspace,
