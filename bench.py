@@ -694,6 +694,10 @@ def main(argv=None):
         ok = True
         if not args.no_verify:
             ok = dec.is_complete() and dec.verify_data(enc)
+        if world > 1:  # the line rank 0 prints speaks for every rank's shard
+            ok_t = torch.tensor([1.0 if ok else 0.0], dtype=torch.float64, device=red_dev)
+            dist.all_reduce(ok_t, op=dist.ReduceOp.MIN)
+            ok = ok_t.item() == 1.0
         steps = args.steps
         out_bytes_step = 2.0 * e * L * B            # parity + recovered, per rank
         value = job_goodput(out_bytes_step, steps, world, elapsed)
