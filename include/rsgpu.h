@@ -157,8 +157,10 @@ size_t rsgpu_decode_workspace_bytes(int k, int e, size_t blocks);
  *               device (isa.cpp:177-204), then the decode rows; any e
  *   GENERATED   the ONE_MATRIX rows baked into per-block straight-line code
  *               (written to executable device memory by the prepare step),
- *               one call per chunk of 8 sources, passes of 32 rows (e <= 63;
- *               AUTO takes it for 32 < e <= 63 too)
+ *               one call per chunk of sources: 2 waves x 16 rows for
+ *               24 < e <= 32 (k_rs_jit16), else waves of 8 rows in passes
+ *               of 32 rows (k_rs_jit; e <= 63; AUTO takes it for
+ *               32 < e <= 63 too)
  * A choice that does not apply to a geometry falls back to GENERAL (e > 32,
  * unaligned rows) or ONE_MATRIX. */
 #define RSGPU_DECODE_AUTO 0

@@ -70,7 +70,7 @@ def regs_of(op):
     return [int(op[1:])]
 
 
-def run_chunk(ins, regs, lds, pending):
+def run_chunk(ins, regs, lds, pending, addr_reg="v20"):
     """Interpret one chunk up to its s_setpc; LDS loads land at issue but stay
     'pending' until an s_waitcnt retires them (reading one is a hazard)."""
     def rd(r):
@@ -91,7 +91,7 @@ def run_chunk(ins, regs, lds, pending):
         elif mnem == "ds_read_b128":
             dst = regs_of(a[0])
             addr, _, rest = a[1].partition(" ")
-            assert addr == "v20", ops
+            assert addr == addr_reg, ops
             o = int(rest.split(":")[1]) if rest else 0
             for i, r in enumerate(dst):
                 regs[r] = lds[o + 4 * i]
@@ -238,3 +238,62 @@ def test_shared_matrix_code(k, e, kind):
         assert n_comp / n_src > 18, n_comp / n_src
     else:
         assert n_comp / n_src < 18, n_comp / n_src
+
+
+def emit16(k, e, coef):
+    import rsgpu
+    f = rsgpu.lib().rsgpu_internal_jit16_emit
+    f.restype = C.c_longlong
+    f.argtypes = [C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_size_t]
+    coef = np.ascontiguousarray(coef, np.uint8)
+    need = f(k, e, coef.ctypes.data, None, 0)
+    assert need > 0
+    out = np.zeros(need, np.uint8)
+    assert f(k, e, coef.ctypes.data, out.ctypes.data, need) == need
+    return out
+
+
+CHUNK_STRIDE16 = 6848  # jit::j16::chunk_stride(): (6 * (112 + 16 * 64) + 8) rounded to 64
+
+
+@pytest.mark.parametrize("k,e", [(64, 32), (25, 25), (100, 30), (13, 27), (218, 32)])
+def test_generated16_block_decodes(k, e):
+    """k_rs_jit16's code (rs_jit.h j16: 2 waves x 16 rows, chunks of 6
+    sources, each source loading its own planes, accumulators v40..v167):
+    every accumulator equals sum_q c[row][q] * src_q over GF(2^8), only the
+    allowed instructions appear, every register is read after its LDS load
+    was waited for, and each chunk returns right after its last source."""
+    rng = random.Random(k * 7 + e)
+    coef = np.array([[rng.randrange(256) for _ in range(k)] for _ in range(e)], np.uint8)
+    coef[1, 2] = 0
+    code = emit16(k, e, coef).tobytes()
+    nch = (k + 5) // 6
+    assert len(code) == 2 * nch * CHUNK_STRIDE16
+    src = [[rng.randrange(256) for _ in range(32)] for _ in range(k)]
+    for w in range(2):
+        nslot = min(16, e - 16 * w)
+        regs = {r: 0 for r in range(256)}
+        pending = []
+        for ch in range(nch):
+            base = (w * nch + ch) * CHUNK_STRIDE16
+            nt = min(6, k - 6 * ch)
+            end = base + nt * (112 + 64 * nslot)
+            ins = disasm(code[base:end + 4])
+            lds = {}
+            for t in range(nt):
+                p = planes(src[6 * ch + t])
+                for a in range(8):
+                    lds[t * 2048 + (a // 4) * 1024 + 4 * (a % 4)] = p[a]
+            ret = run_chunk(ins, regs, lds, pending, addr_reg="v9")
+            assert base + ret == end, "the return sits right after the last source"
+            assert not pending, "a load left outstanding at the return"
+            used = [int(n) for _, _, ops in ins for n in re.findall(r"v\[?(\d+)", ops)]
+            used += [int(n) for _, _, ops in ins for n in re.findall(r"v\[\d+:(\d+)\]", ops)]
+            assert max(used) < 168 and min(used) >= 9, "register outside v9..v167 of k_rs_jit16"
+        for s in range(nslot):
+            row = 16 * w + s
+            want = [0] * 32
+            for q in range(k):
+                want = [x ^ g.gf_mul(int(coef[row, q]), y) for x, y in zip(want, src[q])]
+            got = unplanes([regs[40 + 8 * s + b] for b in range(8)])
+            assert got == want, (k, e, row)
