@@ -12,7 +12,9 @@
 //   hipcc --offload-arch=gfx950 -O3 -std=c++20 -Ibuild_ab \
 //     -Istorage-benchmarks_amd/csrc -Istorage-benchmarks_amd/build \
 //     -o tools/jit16_ab tools/jit16_ab.hip -lhsa-runtime64
-//   tools/jit16_ab [blocks=1024] [reps=5] [check=1] [late=0]
+//   tools/jit16_ab [blocks=1024] [reps=5] [check=1] [late=0] [variants=2]
+// variants: 0 base (k_rs_jit), 1 the tool's 16-row kernel, 2 rs_jit.hip's
+// k_rs_jit16, 3 the same in XCD-contiguous (block, tile) order
 #include "../storage-benchmarks_amd/csrc/rs_jit.hip"
 
 #include <hsa/hsa.h>
@@ -353,12 +355,19 @@ int main(int argc, char** argv)
     a2.chunk_stride = j16::CHUNK_STRIDE;
     a2.block_stride = (long long)per2;
     const dim3 grid((unsigned)((L + 2047) / 2048), (unsigned)B);
+    JitArgs a3 = a2;  // the product kernel (rs_jit.hip k_rs_jit16) in XCD-contiguous order
+    a3.xcd_order = 1;
     auto run = [&](int which) {
         if (which == 0)
             return launch_rs_jit(a, B, 0);
+        if (which == 2)
+            return launch_rs_jit16(a2, B, 0);
+        if (which == 3)
+            return launch_rs_jit16(a3, B, 0);
         hipLaunchKernelGGL(j16::k_jit16, grid, dim3(128), 0, 0, a2);
         return hipGetLastError();
     };
+    const int nvar = argc > 5 ? atoi(argv[5]) : 2;  // variants timed: base, tool rows16, product, product xcd
     if (check) {  // both write the same bytes (the product kernel into the parity rows)
         (void)run(0);
         (void)run(1);
@@ -378,7 +387,7 @@ int main(int argc, char** argv)
         printf("check: %lld differing bytes (sampled blocks)\n", bad);
     }
     for (int rep = 0; rep < R; ++rep)
-        for (int which = 0; which < 2; ++which) {
+        for (int which = 0; which < nvar; ++which) {
             hipEvent_t e0, e1;
             (void)hipEventCreate(&e0);
             (void)hipEventCreate(&e1);
@@ -391,7 +400,8 @@ int main(int argc, char** argv)
             }
             float ms = 0;
             (void)hipEventElapsedTime(&ms, e0, e1);
-            printf("%s rep %d: %.3f ms (%.2f TB/s alg)\n", which ? "rows16" : "base  ", rep, ms,
+            static const char* nm[4] = {"base  ", "rows16", "prod16", "prodx "};
+            printf("%s rep %d: %.3f ms (%.2f TB/s alg)\n", nm[which], rep, ms,
                    (double)B * (k + e) * L / (ms * 1e-3) / 1e12);
         }
     return 0;
