@@ -268,6 +268,10 @@ __device__ __forceinline__ void read_slot16(uint32_t (&W)[8])
 // tile, 168 VGPRs (3 waves per SIMD), sources through LDS in chunks of 6
 // (6 workgroups per CU).  The compiler gets v0..v39; the call clobbers
 // v10..v39 and the accumulators, so what lives across it sits in v0..v8.
+// hipcc warns that v129..v167 in the clobber lists are "reserved": it does
+// not allocate them itself, and the kernel descriptor still gives the wave
+// 168 VGPRs (.amdhsa_next_free_vgpr 168, no AGPRs), which only the asm and
+// the generated code touch.
 __global__ __launch_bounds__(128) __attribute__((amdgpu_num_vgpr(40))) void k_rs_jit16(JitArgs a)
 {
     constexpr int CS = jit::j16::CS;

@@ -63,6 +63,7 @@ int main(int argc, char** argv)
     // operand locality): 0 = as emitted (slot, plane), 1 = by (L, H) operand
     // registers, 2 = by (H, L)
     const int mac_order = argc > 5 ? atoi(argv[5]) : 0;
+    const int xcd = argc > 6 ? atoi(argv[6]) : 0;  // XCD-contiguous (block, tile) order
     const long long L = 1000000, pitch = 1000192;
     uint8_t* rows;
     if (hipMalloc(&rows, (size_t)B * (k + e) * pitch) != hipSuccess) {
@@ -155,6 +156,7 @@ int main(int argc, char** argv)
     a.rows = e;
     a.len = L;
     a.status = d_st;
+    a.xcd_order = xcd;
     for (int rep = 0; rep < 4; ++rep) {  // warm, then measured
         unsigned long long z[8] = {};
         (void)hipMemcpyToSymbol(HIP_SYMBOL(jitk::rsgpu_jit_prof), z, sizeof z);
