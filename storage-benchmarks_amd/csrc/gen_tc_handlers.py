@@ -248,18 +248,19 @@ def main() -> None:
         lines.append(f'#define RSGPU_TC_LOAD_SLOT{slot} "global_load_dwordx4 v[{a0}:{a0 + 3}], %0, off\\n'
                      f'global_load_dwordx4 v[{a0 + 4}:{a0 + 7}], %0, off offset:16\\n"')
     lines.append("#define RSGPU_TC_ACC_CLOBBERS " + ", ".join(f'"v{ACC + i}"' for i in range(64)))
-    # k_rs_jit16 (rs_jit.h j16): 16 rows per wave, 128 accumulators in v40..v167
+    # k_rs_jitw<R> (rs_jit.h Wide): R rows per wave, 8 R accumulators from v40
     A16 = 40
-    lines.append("#define RSGPU_J16_ZERO \\")
-    for i in range(0, 128, 2):
-        lines.append(f'    "v_mov_b64 v[{A16 + i}:{A16 + i + 1}], 0\\n" \\')
-    lines.append("")
+    for R in (16, 10):
+        lines.append(f"#define RSGPU_J{R}_ZERO \\")
+        for i in range(0, 8 * R, 2):
+            lines.append(f'    "v_mov_b64 v[{A16 + i}:{A16 + i + 1}], 0\\n" \\')
+        lines.append("")
+        lines.append(f"#define RSGPU_J{R}_ACC_CLOBBERS " + ", ".join(f'"v{A16 + i}"' for i in range(8 * R)))
     for slot in range(16):
         body = "".join(f"v_mov_b64 %{q}, v[{A16 + 8 * slot + 2 * q}:{A16 + 8 * slot + 2 * q + 1}]\\n"
                        for q in range(4))
-        lines.append(f'#define RSGPU_J16_READ_SLOT64_{slot} "{body}"')
-    lines.append("#define RSGPU_J16_ACC_CLOBBERS " + ", ".join(f'"v{A16 + i}"' for i in range(128)))
-    lines.append("#define RSGPU_J16_CALL_CLOBBERS " + ", ".join(f'"v{r}"' for r in range(10, 40)))
+        lines.append(f'#define RSGPU_JW_READ_SLOT64_{slot} "{body}"')
+    lines.append("#define RSGPU_JW_CALL_CLOBBERS " + ", ".join(f'"v{r}"' for r in range(10, 40)))
     vclob = sorted(set(range(STAGE, STAGE + 8)) | set(TABLE_REGS))
     sclob = list(range(BANK[0], BANK[0] + 16)) + [SM0, RET, RET + 1] + list(range(BANK[1], BANK[1] + 16))
     for ra in RA_LIST:

@@ -181,95 +181,103 @@ RJ_HD inline bool code_word(const uint8_t* rows, int k, int nslot, int ch, int o
     return true;
 }
 
-// ---- 16 rows per wave (k_rs_jit16) ---------------------------------------
+// ---- R rows per wave (k_rs_jitw<R>) ---------------------------------------
 //
-// For 24 < e <= 32 the decode runs as 2 waves x 16 rows per column tile: the
-// composites of a source are built once per 16 rows instead of once per 8
-// (10 % fewer VALU instructions, 40 % fewer instruction-cache misses), at 3
-// waves per SIMD (168 VGPRs) instead of 4.  Register contract:
+// Two waves per column tile, R output rows each, so the composites of a
+// source are built once per R rows instead of once per 8:
+//   R = 16 (k_rs_jit16, 24 < e <= 32): 128 accumulators, 168 VGPRs, 3 waves
+//          per SIMD, chunks of 6 sources (6 workgroups per CU); 10 % fewer
+//          VALU instructions, 40 % fewer instruction-cache misses than 4 x 8
+//   R = 10 (k_rs_jit10, 16 < e <= 20): 80 accumulators, 120 VGPRs, 4 waves
+//          per SIMD, chunks of 5 sources (8 workgroups per CU); composites
+//          twice per source and tile instead of three times (8 + 8 + 4 rows)
+// Register contract (both):
 //   v9             LDS byte address of the chunk's first source + 16 lane
 //   v10..v17       planes of the current source: L1 L2 L4 L8 H1 H2 H4 H8
 //   v18..v28       composites L[n], n = 3 5 6 7 9 ... 15; v29..v39 H[n]
-//   v40..v167      accumulators: slot s (row 16 w + s) plane b at v40+8s+b
+//   v40..v40+8R-1  accumulators: slot s (row R w + s) plane b at v40+8s+b
 //   s[82:83]       return address
-// Code of one chunk (nt <= 6 sources, nslot <= 16 rows of the wave):
+// Code of one chunk (nt <= CS sources, nslot <= R rows of the wave):
 //   source t   ds_read_b128 x2 of its own planes, s_waitcnt lgkmcnt(0), the
 //              22 composites (v_xor_b32), s_nop, then per slot 8
 //              multiply-accumulates (as mac_words)          112 + 64 nslot B
 //   epilogue   s_setpc_b64 s[82:83]; s_nop                           8 B
-// No next-source prefetch (no register bank for it): the other two waves of
-// the SIMD cover the LDS latency.
-namespace j16 {
-constexpr int ADDR = 9, PL = 10, CL = 18, ACC = 40;
-constexpr int CS = 6;          // sources per LDS chunk (2 x 12 KiB: 6 workgroups per CU)
-constexpr int PRE = 112;       // bytes per source before the multiply-accumulates
-RJ_HD constexpr int src_bytes(int nslot) { return PRE + 64 * nslot; }
-RJ_HD constexpr int chunk_stride() { return (CS * src_bytes(16) + 8 + 63) / 64 * 64; }
+// No next-source prefetch (no register bank for it): the other waves of the
+// SIMD cover the LDS latency.
+template <int R_, int CS_>
+struct Wide {
+    static constexpr int R = R_, CS = CS_;
+    static constexpr int ADDR = 9, PL = 10, CL = 18, ACC = 40;
+    static constexpr int PRE = 112;  // bytes per source before the multiply-accumulates
+    RJ_HD static constexpr int src_bytes(int nslot) { return PRE + 64 * nslot; }
+    RJ_HD static constexpr int chunk_stride() { return (CS * src_bytes(R) + 8 + 63) / 64 * 64; }
 
-RJ_HD inline int treg(int hi, int n)
-{
-    if ((n & (n - 1)) == 0) {
-        const int a = n == 1 ? 0 : n == 2 ? 1 : n == 4 ? 2 : 3;
-        return PL + 4 * hi + a;
-    }
-    const int below = 1 + (n > 2) + (n > 4) + (n > 8);
-    return CL + 11 * hi + (n - below - 1);
-}
-
-RJ_HD inline void mac_words(uint8_t c, int s, uint64_t (&wd)[8])
-{
-    for (int b = 0; b < 8; ++b) {
-        const uint8_t m = mat_row(c, b);
-        const int acc = ACC + 8 * s + b, lo = m & 15, hi = m >> 4;
-        wd[b] = lo && hi ? enc_bitop3_96(acc, acc, treg(0, lo), treg(1, hi))
-                : lo     ? enc_xor_e64(acc, acc, treg(0, lo))
-                : hi     ? enc_xor_e64(acc, acc, treg(1, hi))
-                         : (uint64_t)S_NOP0 << 32 | S_NOP0;
-    }
-}
-
-// 32-bit word i (< PRE / 4 = 28) of source t's preamble
-RJ_HD inline uint32_t pre_u32(int t, int i)
-{
-    if (i < 4) {
-        const uint64_t d = enc_ds_read_b128(i < 2 ? PL : PL + 4, ADDR, t * LDS_SRC + (i < 2 ? 0 : LDS_HALF));
-        return (i & 1) ? (uint32_t)(d >> 32) : (uint32_t)d;
-    }
-    if (i == 4)
-        return enc_waitcnt_lgkm(0);
-    const int j = i - 5;
-    if (j >= 22)
-        return S_NOP0;
-    const int hi = j / 11, c = j - 11 * hi;
-    const int n = c < 1 ? 3 : c < 4 ? 4 + c : 5 + c;
-    const int low = n & -n;
-    return enc_xor_e32(treg(hi, n), treg(hi, n ^ low), treg(hi, low));
-}
-
-// Word o (8 bytes) of chunk ch of a wave's code, rows[s * k + q] as in
-// jit::code_word; false past the chunk's return.
-RJ_HD inline bool code_word(const uint8_t* rows, int k, int nslot, int ch, int o, uint64_t* word)
-{
-    const int nt = k - CS * ch < CS ? k - CS * ch : CS;
-    const int per_src = PRE / 8 + 8 * nslot;
-    if (o < nt * per_src) {
-        const int t = o / per_src, r = o - t * per_src;
-        if (r < PRE / 8) {
-            *word = (uint64_t)pre_u32(t, 2 * r + 1) << 32 | pre_u32(t, 2 * r);
-        } else {
-            const int m = r - PRE / 8, s = m >> 3;
-            uint64_t wd[8];
-            mac_words(rows[s * k + CS * ch + t], s, wd);
-            *word = wd[m & 7];
+    RJ_HD static int treg(int hi, int n)
+    {
+        if ((n & (n - 1)) == 0) {
+            const int a = n == 1 ? 0 : n == 2 ? 1 : n == 4 ? 2 : 3;
+            return PL + 4 * hi + a;
         }
-    } else if (o == nt * per_src) {
-        *word = (uint64_t)S_NOP0 << 32 | S_SETPC_82;
-    } else {
-        return false;
+        const int below = 1 + (n > 2) + (n > 4) + (n > 8);
+        return CL + 11 * hi + (n - below - 1);
     }
-    return true;
-}
-}  // namespace j16
+
+    RJ_HD static void mac_words(uint8_t c, int s, uint64_t (&wd)[8])
+    {
+        for (int b = 0; b < 8; ++b) {
+            const uint8_t m = mat_row(c, b);
+            const int acc = ACC + 8 * s + b, lo = m & 15, hi = m >> 4;
+            wd[b] = lo && hi ? enc_bitop3_96(acc, acc, treg(0, lo), treg(1, hi))
+                    : lo     ? enc_xor_e64(acc, acc, treg(0, lo))
+                    : hi     ? enc_xor_e64(acc, acc, treg(1, hi))
+                             : (uint64_t)S_NOP0 << 32 | S_NOP0;
+        }
+    }
+
+    // 32-bit word i (< PRE / 4 = 28) of source t's preamble
+    RJ_HD static uint32_t pre_u32(int t, int i)
+    {
+        if (i < 4) {
+            const uint64_t d = enc_ds_read_b128(i < 2 ? PL : PL + 4, ADDR, t * LDS_SRC + (i < 2 ? 0 : LDS_HALF));
+            return (i & 1) ? (uint32_t)(d >> 32) : (uint32_t)d;
+        }
+        if (i == 4)
+            return enc_waitcnt_lgkm(0);
+        const int j = i - 5;
+        if (j >= 22)
+            return S_NOP0;
+        const int hi = j / 11, c = j - 11 * hi;
+        const int n = c < 1 ? 3 : c < 4 ? 4 + c : 5 + c;
+        const int low = n & -n;
+        return enc_xor_e32(treg(hi, n), treg(hi, n ^ low), treg(hi, low));
+    }
+
+    // Word o (8 bytes) of chunk ch of a wave's code, rows[s * k + q] as in
+    // jit::code_word; false past the chunk's return.
+    RJ_HD static bool code_word(const uint8_t* rows, int k, int nslot, int ch, int o, uint64_t* word)
+    {
+        const int nt = k - CS * ch < CS ? k - CS * ch : CS;
+        const int per_src = PRE / 8 + 8 * nslot;
+        if (o < nt * per_src) {
+            const int t = o / per_src, r = o - t * per_src;
+            if (r < PRE / 8) {
+                *word = (uint64_t)pre_u32(t, 2 * r + 1) << 32 | pre_u32(t, 2 * r);
+            } else {
+                const int m = r - PRE / 8, s = m >> 3;
+                uint64_t wd[8];
+                mac_words(rows[s * k + CS * ch + t], s, wd);
+                *word = wd[m & 7];
+            }
+        } else if (o == nt * per_src) {
+            *word = (uint64_t)S_NOP0 << 32 | S_SETPC_82;
+        } else {
+            return false;
+        }
+        return true;
+    }
+};
+using J16 = Wide<16, 6>;
+using J10 = Wide<10, 5>;
 
 }  // namespace jit
 }  // namespace rsgpu

@@ -236,27 +236,27 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_num_vgpr(64))) void 
 }
 
 template <int S>
-__device__ __forceinline__ void read_slot16(uint32_t (&W)[8])
+__device__ __forceinline__ void read_slotw(uint32_t (&W)[8])
 {
     uint64_t P[4];
-#define RSGPU_J16_RD(TEXT) asm volatile(TEXT : "=v"(P[0]), "=v"(P[1]), "=v"(P[2]), "=v"(P[3]))
-    if constexpr (S == 0) RSGPU_J16_RD(RSGPU_J16_READ_SLOT64_0);
-    if constexpr (S == 1) RSGPU_J16_RD(RSGPU_J16_READ_SLOT64_1);
-    if constexpr (S == 2) RSGPU_J16_RD(RSGPU_J16_READ_SLOT64_2);
-    if constexpr (S == 3) RSGPU_J16_RD(RSGPU_J16_READ_SLOT64_3);
-    if constexpr (S == 4) RSGPU_J16_RD(RSGPU_J16_READ_SLOT64_4);
-    if constexpr (S == 5) RSGPU_J16_RD(RSGPU_J16_READ_SLOT64_5);
-    if constexpr (S == 6) RSGPU_J16_RD(RSGPU_J16_READ_SLOT64_6);
-    if constexpr (S == 7) RSGPU_J16_RD(RSGPU_J16_READ_SLOT64_7);
-    if constexpr (S == 8) RSGPU_J16_RD(RSGPU_J16_READ_SLOT64_8);
-    if constexpr (S == 9) RSGPU_J16_RD(RSGPU_J16_READ_SLOT64_9);
-    if constexpr (S == 10) RSGPU_J16_RD(RSGPU_J16_READ_SLOT64_10);
-    if constexpr (S == 11) RSGPU_J16_RD(RSGPU_J16_READ_SLOT64_11);
-    if constexpr (S == 12) RSGPU_J16_RD(RSGPU_J16_READ_SLOT64_12);
-    if constexpr (S == 13) RSGPU_J16_RD(RSGPU_J16_READ_SLOT64_13);
-    if constexpr (S == 14) RSGPU_J16_RD(RSGPU_J16_READ_SLOT64_14);
-    if constexpr (S == 15) RSGPU_J16_RD(RSGPU_J16_READ_SLOT64_15);
-#undef RSGPU_J16_RD
+#define RSGPU_JW_RD(TEXT) asm volatile(TEXT : "=v"(P[0]), "=v"(P[1]), "=v"(P[2]), "=v"(P[3]))
+    if constexpr (S == 0) RSGPU_JW_RD(RSGPU_JW_READ_SLOT64_0);
+    if constexpr (S == 1) RSGPU_JW_RD(RSGPU_JW_READ_SLOT64_1);
+    if constexpr (S == 2) RSGPU_JW_RD(RSGPU_JW_READ_SLOT64_2);
+    if constexpr (S == 3) RSGPU_JW_RD(RSGPU_JW_READ_SLOT64_3);
+    if constexpr (S == 4) RSGPU_JW_RD(RSGPU_JW_READ_SLOT64_4);
+    if constexpr (S == 5) RSGPU_JW_RD(RSGPU_JW_READ_SLOT64_5);
+    if constexpr (S == 6) RSGPU_JW_RD(RSGPU_JW_READ_SLOT64_6);
+    if constexpr (S == 7) RSGPU_JW_RD(RSGPU_JW_READ_SLOT64_7);
+    if constexpr (S == 8) RSGPU_JW_RD(RSGPU_JW_READ_SLOT64_8);
+    if constexpr (S == 9) RSGPU_JW_RD(RSGPU_JW_READ_SLOT64_9);
+    if constexpr (S == 10) RSGPU_JW_RD(RSGPU_JW_READ_SLOT64_10);
+    if constexpr (S == 11) RSGPU_JW_RD(RSGPU_JW_READ_SLOT64_11);
+    if constexpr (S == 12) RSGPU_JW_RD(RSGPU_JW_READ_SLOT64_12);
+    if constexpr (S == 13) RSGPU_JW_RD(RSGPU_JW_READ_SLOT64_13);
+    if constexpr (S == 14) RSGPU_JW_RD(RSGPU_JW_READ_SLOT64_14);
+    if constexpr (S == 15) RSGPU_JW_RD(RSGPU_JW_READ_SLOT64_15);
+#undef RSGPU_JW_RD
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         W[2 * q] = (uint32_t)P[q];
@@ -264,17 +264,19 @@ __device__ __forceinline__ void read_slot16(uint32_t (&W)[8])
     }
 }
 
-// The same decode with 16 rows per wave (rs_jit.h j16): 2 waves per column
-// tile, 168 VGPRs (3 waves per SIMD), sources through LDS in chunks of 6
-// (6 workgroups per CU).  The compiler gets v0..v39; the call clobbers
+// The same decode with R rows per wave (rs_jit.h Wide): 2 waves per column
+// tile; R = 16: 168 VGPRs (3 waves per SIMD), chunks of 6 sources (6
+// workgroups per CU); R = 10: 120 VGPRs (4 waves per SIMD), chunks of 5 (8
+// workgroups per CU).  The compiler gets v0..v39; the call clobbers
 // v10..v39 and the accumulators, so what lives across it sits in v0..v8.
 // hipcc warns that v129..v167 in the clobber lists are "reserved": it does
 // not allocate them itself, and the kernel descriptor still gives the wave
 // 168 VGPRs (.amdhsa_next_free_vgpr 168, no AGPRs), which only the asm and
 // the generated code touch.
-__global__ __launch_bounds__(128) __attribute__((amdgpu_num_vgpr(40))) void k_rs_jit16(JitArgs a)
+template <class W>
+__global__ __launch_bounds__(128) __attribute__((amdgpu_num_vgpr(40))) void k_rs_jitw(JitArgs a)
 {
-    constexpr int CS = jit::j16::CS;
+    constexpr int CS = W::CS, R = W::R;
     __shared__ uint4 lds[2][CS * 2 * 64];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
@@ -305,7 +307,10 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_num_vgpr(40))) void k_rs
         for (int t = wave; t < nt; t += 2)
             glds32(sload_ptr(srcs + c0 + t), loff, base + (uint32_t)(t * 2 * 64 * 16));
     };
-    asm volatile(RSGPU_J16_ZERO ::: RSGPU_J16_ACC_CLOBBERS);
+    if constexpr (R == 16)
+        asm volatile(RSGPU_J16_ZERO ::: RSGPU_J16_ACC_CLOBBERS);
+    else
+        asm volatile(RSGPU_J10_ZERO ::: RSGPU_J10_ACC_CLOBBERS);
     issue(0);
     for (int ch = 0; ch < nch; ++ch) {
         const int nt = min(CS, k - ch * CS);
@@ -315,10 +320,10 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_num_vgpr(40))) void k_rs
             const uint32_t m4 = vconst(0x0F0F0F0Fu), m2 = vconst(0x33333333u), m1 = vconst(0x55555555u);
             for (int t = wave; t < nt; t += 2) {
                 uint4 u = buf[(t * 2 + 0) * 64 + lane], v = buf[(t * 2 + 1) * 64 + lane];
-                uint32_t W[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
-                tr8(W, m4, m2, m1);
-                buf[(t * 2 + 0) * 64 + lane] = make_uint4(W[0], W[1], W[2], W[3]);
-                buf[(t * 2 + 1) * 64 + lane] = make_uint4(W[4], W[5], W[6], W[7]);
+                uint32_t Wd[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
+                tr8(Wd, m4, m2, m1);
+                buf[(t * 2 + 0) * 64 + lane] = make_uint4(Wd[0], Wd[1], Wd[2], Wd[3]);
+                buf[(t * 2 + 1) * 64 + lane] = make_uint4(Wd[4], Wd[5], Wd[6], Wd[7]);
             }
         }
         barrier_lds();
@@ -326,26 +331,32 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_num_vgpr(40))) void k_rs
             issue(ch + 1);
         const uint32_t la = lds0 + (uint32_t)((ch & 1) * CS * 2 * 64 * 16) + lane * 16;
         const uint8_t* fn = code + (size_t)ch * a.chunk_stride;
-        asm volatile("s_swappc_b64 s[82:83], %[fn]"
-                     :
-                     : [fn] "s"(fn), "{v9}"(la)
-                     : RSGPU_J16_CALL_CLOBBERS, "s82", "s83", "scc", "memory", RSGPU_J16_ACC_CLOBBERS);
+        if constexpr (R == 16)
+            asm volatile("s_swappc_b64 s[82:83], %[fn]"
+                         :
+                         : [fn] "s"(fn), "{v9}"(la)
+                         : RSGPU_JW_CALL_CLOBBERS, "s82", "s83", "scc", "memory", RSGPU_J16_ACC_CLOBBERS);
+        else
+            asm volatile("s_swappc_b64 s[82:83], %[fn]"
+                         :
+                         : [fn] "s"(fn), "{v9}"(la)
+                         : RSGPU_JW_CALL_CLOBBERS, "s82", "s83", "scc", "memory", RSGPU_J10_ACC_CLOBBERS);
     }
     if (off + 32 <= a.len) {
         const uint32_t m4 = vconst(0x0F0F0F0Fu), m2 = vconst(0x33333333u), m1 = vconst(0x55555555u);
         [&]<int... Ss>(std::integer_sequence<int, Ss...>) {
             (
                 [&] {
-                    const int r = wave * 16 + Ss;
+                    const int r = wave * R + Ss;
                     if (r < a.rows) {
-                        uint32_t W[8];
-                        read_slot16<Ss>(W);
-                        tr8(W, m4, m2, m1);
-                        store32((uint8_t*)sload_ptr((const uint8_t* const*)(dsts + r)), off, W);
+                        uint32_t Wd[8];
+                        read_slotw<Ss>(Wd);
+                        tr8(Wd, m4, m2, m1);
+                        store32((uint8_t*)sload_ptr((const uint8_t* const*)(dsts + r)), off, Wd);
                     }
                 }(),
                 ...);
-        }(std::make_integer_sequence<int, 16>{});
+        }(std::make_integer_sequence<int, R>{});
     }
 }
 
@@ -414,74 +425,89 @@ __global__ __launch_bounds__(256) void k_jit_emit(int k, int e, const uint8_t* c
     }
 }
 
-// k_rs_jit16's code (rs_jit.h j16), one workgroup per (block, wave) as
-// k_jit_emit: rows 16 w .. 16 w + 15 of the block's decode rows
-__global__ __launch_bounds__(256) void k_jit16_emit(int k, int e, const uint8_t* coef, const int* status,
-                                                    uint8_t* code)
+// k_rs_jitw<R>'s code (rs_jit.h Wide), one workgroup per (block, wave) as
+// k_jit_emit: rows R w .. R w + R - 1 of the block's decode rows
+template <class W>
+__global__ __launch_bounds__(256) void k_jitw_emit(int k, int e, const uint8_t* coef, const int* status,
+                                                   uint8_t* code)
 {
-    namespace J = jit::j16;
-    __shared__ uint8_t cw[16 * 256];
+    constexpr int R = W::R, CS = W::CS;
+    __shared__ uint8_t cw[R * 256];
     const int b = blockIdx.y, w = blockIdx.x;
     if (status[b] != 0)
         return;
-    const int nch = (k + J::CS - 1) / J::CS;
-    const int nslot = min(16, e - 16 * w);
-    const size_t stride = (size_t)J::chunk_stride();
+    const int nch = (k + CS - 1) / CS;
+    const int nslot = min(R, e - R * w);
+    const size_t stride = (size_t)W::chunk_stride();
     uint8_t* cbase = code + ((size_t)b * 2 + w) * nch * stride;
-    const int sb = J::src_bytes(nslot);
+    const int sb = W::src_bytes(nslot);
     for (int i = threadIdx.x; i < nslot * k; i += blockDim.x)
-        cw[i] = coef[((size_t)b * e + 16 * w) * k + i];
+        cw[i] = coef[((size_t)b * e + R * w) * k + i];
     __syncthreads();
-    for (int i = threadIdx.x; i < 16 * k; i += blockDim.x) {  // (source, slot) runs
-        const int q = i >> 4, s = i & 15;
+    for (int i = threadIdx.x; i < R * k; i += blockDim.x) {  // (source, slot) runs
+        const int q = i / R, s = i - q * R;
         if (s >= nslot)
             continue;
-        const int ch = q / J::CS, t = q - ch * J::CS;
+        const int ch = q / CS, t = q - ch * CS;
         uint64_t wd[8];
-        J::mac_words(cw[s * k + q], s, wd);
-        uint4* dst = reinterpret_cast<uint4*>(cbase + (size_t)ch * stride + (size_t)t * sb + J::PRE + 64 * s);
+        W::mac_words(cw[s * k + q], s, wd);
+        uint4* dst = reinterpret_cast<uint4*>(cbase + (size_t)ch * stride + (size_t)t * sb + W::PRE + 64 * s);
 #pragma unroll
         for (int j = 0; j < 4; ++j)
             dst[j] = make_uint4((uint32_t)wd[2 * j], (uint32_t)(wd[2 * j] >> 32), (uint32_t)wd[2 * j + 1],
                                 (uint32_t)(wd[2 * j + 1] >> 32));
     }
-    constexpr int PW = J::PRE / 8;
+    constexpr int PW = W::PRE / 8;
     for (int i = threadIdx.x; i < PW * k; i += blockDim.x) {  // preambles
         const int q = i / PW, r = i - q * PW;
-        const int ch = q / J::CS, t = q - ch * J::CS;
+        const int ch = q / CS, t = q - ch * CS;
         reinterpret_cast<uint64_t*>(cbase + (size_t)ch * stride + (size_t)t * sb)[r] =
-            (uint64_t)J::pre_u32(t, 2 * r + 1) << 32 | J::pre_u32(t, 2 * r);
+            (uint64_t)W::pre_u32(t, 2 * r + 1) << 32 | W::pre_u32(t, 2 * r);
     }
     for (int ch = threadIdx.x; ch < nch; ch += blockDim.x) {  // returns
-        const int nt = min(J::CS, k - J::CS * ch);
+        const int nt = min(CS, k - CS * ch);
         reinterpret_cast<uint64_t*>(cbase + (size_t)ch * stride)[nt * (PW + 8 * nslot)] =
             (uint64_t)jit::S_NOP0 << 32 | jit::S_SETPC_82;
     }
 }
 
-bool jit16_rows(int e) { return e > 24 && e <= 32; }
+// rows per wave of the 2-wave layout for e rows, 0 = the 8-row layout
+int jitw_rows(int e) { return e > 24 && e <= 32 ? 16 : e > 16 && e <= 20 ? 10 : 0; }
 
-size_t jit16_code_bytes(int k, long long blocks)
+size_t jitw_chunk_stride(int e)
 {
-    const int nch = (k + jit::j16::CS - 1) / jit::j16::CS;
-    return (size_t)blocks * 2 * nch * jit::j16::chunk_stride();
+    return jitw_rows(e) == 16 ? jit::J16::chunk_stride() : jit::J10::chunk_stride();
 }
 
-hipError_t launch_jit16_emit(int k, int e, long long blocks, const uint8_t* coef, const int* status,
-                             uint8_t* code, hipStream_t st)
+size_t jitw_code_bytes(int k, int e, long long blocks)
 {
-    if (k <= 0 || k > 250 || !jit16_rows(e) || k + e > 250 || blocks <= 0 || !coef || !status || !code)
+    const int cs = jitw_rows(e) == 16 ? jit::J16::CS : jit::J10::CS;
+    return (size_t)blocks * 2 * ((k + cs - 1) / cs) * jitw_chunk_stride(e);
+}
+
+hipError_t launch_jitw_emit(int k, int e, long long blocks, const uint8_t* coef, const int* status,
+                            uint8_t* code, hipStream_t st)
+{
+    if (k <= 0 || k > 250 || !jitw_rows(e) || k + e > 250 || blocks <= 0 || !coef || !status || !code)
         return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_jit16_emit, dim3(2, (unsigned)blocks), dim3(256), 0, st, k, e, coef, status, code);
+    if (jitw_rows(e) == 16)
+        hipLaunchKernelGGL(k_jitw_emit<jit::J16>, dim3(2, (unsigned)blocks), dim3(256), 0, st, k, e, coef, status,
+                           code);
+    else
+        hipLaunchKernelGGL(k_jitw_emit<jit::J10>, dim3(2, (unsigned)blocks), dim3(256), 0, st, k, e, coef, status,
+                           code);
     return hipGetLastError();
 }
 
-hipError_t launch_rs_jit16(const JitArgs& a, long long blocks, hipStream_t st)
+hipError_t launch_rs_jitw(const JitArgs& a, long long blocks, hipStream_t st)
 {
-    if (!jit16_rows(a.rows) || a.dst_stride < a.rows || a.k <= 0 || !a.code || a.chunk_stride <= 0)
+    if (!jitw_rows(a.rows) || a.dst_stride < a.rows || a.k <= 0 || !a.code || a.chunk_stride <= 0)
         return hipErrorInvalidValue;
     dim3 grid((unsigned)((a.len + 2047) / 2048), (unsigned)blocks);
-    hipLaunchKernelGGL(jitk::k_rs_jit16, grid, dim3(128), 0, st, a);
+    if (jitw_rows(a.rows) == 16)
+        hipLaunchKernelGGL(jitk::k_rs_jitw<jit::J16>, grid, dim3(128), 0, st, a);
+    else
+        hipLaunchKernelGGL(jitk::k_rs_jitw<jit::J10>, grid, dim3(128), 0, st, a);
     return hipGetLastError();
 }
 

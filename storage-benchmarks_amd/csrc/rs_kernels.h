@@ -116,14 +116,15 @@ hipError_t launch_jit_emit(int k, int e, long long blocks, const uint8_t* coef, 
                            uint8_t* code, hipStream_t st);
 hipError_t launch_jit_fill(void* code, size_t bytes, hipStream_t st);
 hipError_t launch_rs_jit(const JitArgs& a, long long blocks, hipStream_t st);
-// 16 rows per wave (rs_jit.h j16) for 24 < e <= 32: code of block b, wave w
-// (of 2), chunk ch (of 6 sources) at code + ((b 2 + w) nch6 + ch)
-// jit::j16::chunk_stride()
-bool jit16_rows(int e);
-size_t jit16_code_bytes(int k, long long blocks);
-hipError_t launch_jit16_emit(int k, int e, long long blocks, const uint8_t* coef, const int* status,
-                             uint8_t* code, hipStream_t st);
-hipError_t launch_rs_jit16(const JitArgs& a, long long blocks, hipStream_t st);
+// Two waves of R rows per tile (rs_jit.h Wide): R = jitw_rows(e) (16 for
+// 24 < e <= 32, 10 for 16 < e <= 20, else 0 = not this layout); code of
+// block b, wave w, chunk ch at code + ((b 2 + w) nch + ch) jitw_chunk_stride(e)
+int jitw_rows(int e);
+size_t jitw_chunk_stride(int e);
+size_t jitw_code_bytes(int k, int e, long long blocks);
+hipError_t launch_jitw_emit(int k, int e, long long blocks, const uint8_t* coef, const int* status,
+                            uint8_t* code, hipStream_t st);
+hipError_t launch_rs_jitw(const JitArgs& a, long long blocks, hipStream_t st);
 // device-to-device copy into executable memory (host-built code staged in
 // ordinary device memory first), bytes % 8 == 0
 hipError_t launch_jit_copy(void* dst, const void* src, size_t bytes, hipStream_t st);

@@ -1044,23 +1044,25 @@ WsLayout ws_layout(int k, int e, size_t blocks)
     return w;
 }
 
-// Generated decode code of a call: 16 rows per wave for 24 < e <= 32 (two
-// balanced waves, rs_jit.h j16), else 8 rows per wave in passes of 32.
-// Measured on the same boxes (tools/jit16_ab.hip, profiles/r02_ab/jit_rows16):
-// 10 % fewer VALU instructions, 40 % fewer instruction-cache misses, 3 % more
-// cycles at 3 waves per SIMD; 0-4 % faster.
+// Generated decode code of a call: two waves of 16 rows for 24 < e <= 32 or
+// of 10 rows for 16 < e <= 20 (rs_jit.h Wide: the composites of a source
+// built twice per tile instead of 4 or 3 times), else waves of 8 rows in
+// passes of 32.  k_rs_jit16 measured on the same boxes (tools/jit16_ab.hip,
+// profiles/r02_ab/jit_rows16): 10 % fewer VALU instructions, 40 % fewer
+// instruction-cache misses, 3 % more cycles at 3 waves per SIMD; with the
+// XCD-contiguous order 3.7 % faster than the 8-row kernel.
 size_t decode_code_bytes(int k, int e, size_t blocks)
 {
-    return jit16_rows(e) ? jit16_code_bytes(k, (long long)blocks) : jit_code_bytes(k, e, (long long)blocks);
+    return jitw_rows(e) ? jitw_code_bytes(k, e, (long long)blocks) : jit_code_bytes(k, e, (long long)blocks);
 }
 
-// k_jit_emit / k_jit16_emit: the code of every block from its decode rows
+// k_jit_emit / k_jitw_emit: the code of every block from its decode rows
 // coef [B][e][k] into the context's executable memory
 int emit_decode_code(rsgpu_ctx* ctx, int k, int e, size_t blocks, const uint8_t* coef, const int* d_status)
 {
-    if (jit16_rows(e)) {
-        KTimer ke(ctx, "k_jit16_emit", blocks);
-        RS_HIP(ctx, launch_jit16_emit(k, e, (long long)blocks, coef, d_status, (uint8_t*)ctx->d_jit, ctx->stream));
+    if (jitw_rows(e)) {
+        KTimer ke(ctx, jitw_rows(e) == 16 ? "k_jit16_emit" : "k_jit10_emit", blocks);
+        RS_HIP(ctx, launch_jitw_emit(k, e, (long long)blocks, coef, d_status, (uint8_t*)ctx->d_jit, ctx->stream));
     } else {
         KTimer ke(ctx, "k_jit_emit", blocks);
         RS_HIP(ctx, launch_jit_emit(k, e, (long long)blocks, coef, d_status, (uint8_t*)ctx->d_jit, ctx->stream));
@@ -1069,7 +1071,7 @@ int emit_decode_code(rsgpu_ctx* ctx, int k, int e, size_t blocks, const uint8_t*
 }
 
 // The per-block generated decode (rs_jit.hip) over rows e of every block:
-// k_rs_jit16 in one launch (decode_code_bytes), or k_rs_jit in passes of
+// k_rs_jitw in one launch (decode_code_bytes), or k_rs_jit in passes of
 // <= 32 rows: block b, pass p, wave w, chunk ch at d_jit + b block_stride +
 // ((4 p + w) nch + ch) chunk_stride (k_jit_emit's layout).
 int jit_decode_launch(rsgpu_ctx* ctx, int k, int e, size_t len, size_t blocks,
@@ -1077,26 +1079,25 @@ int jit_decode_launch(rsgpu_ctx* ctx, int k, int e, size_t len, size_t blocks,
 {
     if (!ctx->d_jit || ctx->jit_bytes < decode_code_bytes(k, e, blocks))
         return fail(ctx, RSGPU_ERR_ARG, "rsgpu_decode_apply: no prepared decode code");
-    if (jit16_rows(e)) {
-        const int nch = (k + jit::j16::CS - 1) / jit::j16::CS;
+    if (jitw_rows(e)) {
         JitArgs j{};
         j.srcs = d_srcs;
         j.dsts = d_dsts;
         j.code = (const uint8_t*)ctx->d_jit;
-        j.chunk_stride = jit::j16::chunk_stride();
-        j.block_stride = (long long)2 * nch * jit::j16::chunk_stride();
+        j.chunk_stride = (long long)jitw_chunk_stride(e);
+        j.block_stride = (long long)jitw_code_bytes(k, e, 1);
         j.k = k;
         j.rows = e;
         j.dst_stride = e;
         j.len = (long long)len;
         j.status = d_status;
         // each XCD a contiguous range of (block, tile): a block's code is
-        // fetched into one L2, not eight -- 3.7 % faster at C3 for this
-        // kernel (23.3 vs 24.2 ms, profiles/r02_ab/jit_rows16/xcd_*.log),
+        // fetched into one L2, not eight -- 3.7 % faster at C3 for the
+        // 16-row kernel (23.3 vs 24.2 ms, profiles/r02_ab/jit_rows16/xcd_*.log),
         // where the 8-row kernel measured 1 % slower
         j.xcd_order = 1;
-        KTimer kt(ctx, "k_rs_jit16(decode)", blocks);
-        RS_HIP(ctx, launch_rs_jit16(j, (long long)blocks, ctx->stream));
+        KTimer kt(ctx, jitw_rows(e) == 16 ? "k_rs_jit16(decode)" : "k_rs_jit10(decode)", blocks);
+        RS_HIP(ctx, launch_rs_jitw(j, (long long)blocks, ctx->stream));
         return RSGPU_OK;
     }
     const int nch = (k + 7) / 8, nwt = (e + 7) / 8;
@@ -1467,31 +1468,40 @@ long long rsgpu_internal_jit_emit(int k, int e, const unsigned char* coef, unsig
     return (long long)need;
 }
 
-// Test hook (not part of include/rsgpu.h): the same for the 16-rows-per-wave
-// layout of k_rs_jit16 (rs_jit.h j16, 24 < e <= 32), from jit::j16::code_word
-// (the words k_jit16_emit writes).
-long long rsgpu_internal_jit16_emit(int k, int e, const unsigned char* coef, unsigned char* out,
-                                    size_t out_bytes)
+// Test hook (not part of include/rsgpu.h): the same for the two-wave layouts
+// of k_rs_jitw (rs_jit.h Wide, R = 16 for 24 < e <= 32, 10 for 16 < e <= 20),
+// from Wide::code_word (the words k_jitw_emit writes).
+extern "C++" template <class W>
+static void jitw_emit_host(int k, int e, const unsigned char* coef, uint64_t* o64)
 {
-    if (k <= 0 || !jit16_rows(e) || k + e > 250 || !coef)
-        return -1;
-    const size_t need = jit16_code_bytes(k, 1);
-    if (!out || out_bytes < need)
-        return (long long)need;
-    const int nch = (k + jit::j16::CS - 1) / jit::j16::CS, stride_w = jit::j16::chunk_stride() / 8;
-    uint64_t* o64 = reinterpret_cast<uint64_t*>(out);
-    for (size_t i = 0; i < need / 8; ++i)
-        o64[i] = (uint64_t)jit::S_NOP0 << 32 | jit::S_SETPC_82;
+    const int nch = (k + W::CS - 1) / W::CS, stride_w = W::chunk_stride() / 8;
     for (int w = 0; w < 2; ++w) {
-        const int nslot = std::min(16, e - 16 * w);
-        const unsigned char* rows = coef + (size_t)16 * w * k;
+        const int nslot = std::min(W::R, e - W::R * w);
+        const unsigned char* rows = coef + (size_t)W::R * w * k;
         for (int ch = 0; ch < nch; ++ch)
             for (int o = 0; o < stride_w; ++o) {
                 uint64_t word;
-                if (jit::j16::code_word(rows, k, nslot, ch, o, &word))
+                if (W::code_word(rows, k, nslot, ch, o, &word))
                     o64[((size_t)w * nch + ch) * stride_w + o] = word;
             }
     }
+}
+
+long long rsgpu_internal_jitw_emit(int k, int e, const unsigned char* coef, unsigned char* out,
+                                   size_t out_bytes)
+{
+    if (k <= 0 || !jitw_rows(e) || k + e > 250 || !coef)
+        return -1;
+    const size_t need = jitw_code_bytes(k, e, 1);
+    if (!out || out_bytes < need)
+        return (long long)need;
+    uint64_t* o64 = reinterpret_cast<uint64_t*>(out);
+    for (size_t i = 0; i < need / 8; ++i)
+        o64[i] = (uint64_t)jit::S_NOP0 << 32 | jit::S_SETPC_82;
+    if (jitw_rows(e) == 16)
+        jitw_emit_host<jit::J16>(k, e, coef, o64);
+    else
+        jitw_emit_host<jit::J10>(k, e, coef, o64);
     return (long long)need;
 }
 

@@ -87,8 +87,10 @@ GEOMS = [(16, 4, 1000000, 2), (64, 32, 1000000, 2), (100, 20, 1000000, 2), (16, 
          (12, 12, 512, 2), (33, 1, 64, 2),
          # 32 < e <= 63: closed-form rows, generated code in passes of 32 rows
          (96, 48, 131072, 2), (187, 63, 4096, 2), (40, 33, 98304, 2),
-         # 24 < e <= 32: 16 rows per wave (k_rs_jit16) when generated
-         (50, 25, 98304, 3), (31, 31, 4096, 2), (218, 32, 2048, 2)]
+         # 24 < e <= 32: 16 rows per wave (k_rs_jit16) when generated;
+         # 16 < e <= 20: 10 rows per wave (k_rs_jit10)
+         (50, 25, 98304, 3), (31, 31, 4096, 2), (218, 32, 2048, 2),
+         (17, 17, 65536, 2), (64, 19, 4096, 3), (230, 20, 2048, 2)]
 
 
 @pytest.mark.parametrize("kernel", KERNELS)

@@ -240,9 +240,9 @@ def test_shared_matrix_code(k, e, kind):
         assert n_comp / n_src < 18, n_comp / n_src
 
 
-def emit16(k, e, coef):
+def emitw(k, e, coef):
     import rsgpu
-    f = rsgpu.lib().rsgpu_internal_jit16_emit
+    f = rsgpu.lib().rsgpu_internal_jitw_emit
     f.restype = C.c_longlong
     f.argtypes = [C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_size_t]
     coef = np.ascontiguousarray(coef, np.uint8)
@@ -253,35 +253,40 @@ def emit16(k, e, coef):
     return out
 
 
-CHUNK_STRIDE16 = 6848  # jit::j16::chunk_stride(): (6 * (112 + 16 * 64) + 8) rounded to 64
+# Wide<R, CS>::chunk_stride(): (CS * (112 + 64 R) + 8) rounded to 64
+WIDE = {16: (6, 6848), 10: (5, 3776)}
 
 
-@pytest.mark.parametrize("k,e", [(64, 32), (25, 25), (100, 30), (13, 27), (218, 32)])
-def test_generated16_block_decodes(k, e):
-    """k_rs_jit16's code (rs_jit.h j16: 2 waves x 16 rows, chunks of 6
-    sources, each source loading its own planes, accumulators v40..v167):
-    every accumulator equals sum_q c[row][q] * src_q over GF(2^8), only the
-    allowed instructions appear, every register is read after its LDS load
-    was waited for, and each chunk returns right after its last source."""
+@pytest.mark.parametrize("k,e", [(64, 32), (25, 25), (100, 30), (13, 27), (218, 32),
+                                 (100, 20), (17, 17), (64, 19), (230, 20)])
+def test_generated_wide_block_decodes(k, e):
+    """k_rs_jitw's code (rs_jit.h Wide: 2 waves x R rows, R = 16 for
+    24 < e <= 32 and 10 for 16 < e <= 20, chunks of CS sources, each source
+    loading its own planes, accumulators from v40): every accumulator equals
+    sum_q c[row][q] * src_q over GF(2^8), only the allowed instructions
+    appear, every register is read after its LDS load was waited for, and
+    each chunk returns right after its last source."""
+    R = 16 if e > 24 else 10
+    cs, stride = WIDE[R]
     rng = random.Random(k * 7 + e)
     coef = np.array([[rng.randrange(256) for _ in range(k)] for _ in range(e)], np.uint8)
     coef[1, 2] = 0
-    code = emit16(k, e, coef).tobytes()
-    nch = (k + 5) // 6
-    assert len(code) == 2 * nch * CHUNK_STRIDE16
+    code = emitw(k, e, coef).tobytes()
+    nch = (k + cs - 1) // cs
+    assert len(code) == 2 * nch * stride
     src = [[rng.randrange(256) for _ in range(32)] for _ in range(k)]
     for w in range(2):
-        nslot = min(16, e - 16 * w)
+        nslot = min(R, e - R * w)
         regs = {r: 0 for r in range(256)}
         pending = []
         for ch in range(nch):
-            base = (w * nch + ch) * CHUNK_STRIDE16
-            nt = min(6, k - 6 * ch)
+            base = (w * nch + ch) * stride
+            nt = min(cs, k - cs * ch)
             end = base + nt * (112 + 64 * nslot)
             ins = disasm(code[base:end + 4])
             lds = {}
             for t in range(nt):
-                p = planes(src[6 * ch + t])
+                p = planes(src[cs * ch + t])
                 for a in range(8):
                     lds[t * 2048 + (a // 4) * 1024 + 4 * (a % 4)] = p[a]
             ret = run_chunk(ins, regs, lds, pending, addr_reg="v9")
@@ -289,9 +294,9 @@ def test_generated16_block_decodes(k, e):
             assert not pending, "a load left outstanding at the return"
             used = [int(n) for _, _, ops in ins for n in re.findall(r"v\[?(\d+)", ops)]
             used += [int(n) for _, _, ops in ins for n in re.findall(r"v\[\d+:(\d+)\]", ops)]
-            assert max(used) < 168 and min(used) >= 9, "register outside v9..v167 of k_rs_jit16"
+            assert max(used) < 40 + 8 * R and min(used) >= 9, "register outside the kernel's v9..v(40+8R-1)"
         for s in range(nslot):
-            row = 16 * w + s
+            row = R * w + s
             want = [0] * 32
             for q in range(k):
                 want = [x ^ g.gf_mul(int(coef[row, q]), y) for x, y in zip(want, src[q])]

@@ -14,7 +14,7 @@
 //     -o tools/jit16_ab tools/jit16_ab.hip -lhsa-runtime64
 //   tools/jit16_ab [blocks=1024] [reps=5] [check=1] [late=0] [variants=2]
 // variants: 0 base (k_rs_jit), 1 the tool's 16-row kernel, 2 rs_jit.hip's
-// k_rs_jit16, 3 the same in XCD-contiguous (block, tile) order
+// k_rs_jitw<16>, 3 the same in XCD-contiguous (block, tile) order
 #include "../storage-benchmarks_amd/csrc/rs_jit.hip"
 
 #include <hsa/hsa.h>
@@ -361,9 +361,9 @@ int main(int argc, char** argv)
         if (which == 0)
             return launch_rs_jit(a, B, 0);
         if (which == 2)
-            return launch_rs_jit16(a2, B, 0);
+            return launch_rs_jitw(a2, B, 0);
         if (which == 3)
-            return launch_rs_jit16(a3, B, 0);
+            return launch_rs_jitw(a3, B, 0);
         hipLaunchKernelGGL(j16::k_jit16, grid, dim3(128), 0, 0, a2);
         return hipGetLastError();
     };

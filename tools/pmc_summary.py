@@ -7,8 +7,8 @@ from collections import defaultdict
 
 
 def short(k: str) -> str:
-    if "k_rs_jit16" in k:
-        return "k_rs_jit16(decode)"
+    if "k_rs_jitw" in k:  # rs_jit.h Wide<R, CS>
+        return "k_rs_jit16(decode)" if "Wide<16" in k else "k_rs_jit10(decode)"
     if "k_rs_jit" in k:  # <NW, true>: the shared-program encode
         return "k_rs_jit(encode)" if "true>" in k.split("(")[0] else "k_rs_jit(decode)"
     for key in ("k_rs_decode_fused", "k_rs_tc", "k_rs_jit", "k_rs_bs", "k_dot_generic",

@@ -18,8 +18,8 @@ def name_of(kernel: str) -> str:
         return "k_rs_bs(syndrome)" if kernel.split(">")[0].rstrip().endswith("true") else "k_rs_bs(encode)"
     if "k_rs_decode_fused" in kernel:
         return "k_rs_decode_fused"
-    if "k_rs_jit16" in kernel:
-        return "k_rs_jit16(decode)"
+    if "k_rs_jitw" in kernel:  # rs_jit.h Wide<R, CS>
+        return "k_rs_jit16(decode)" if "Wide<16" in kernel else "k_rs_jit10(decode)"
     if "k_rs_jit" in kernel:
         return "k_rs_jit(encode)" if "true>" in kernel.split("(")[0] else "k_rs_jit(decode)"
     if "k_rs_tc" in kernel:  # the bench's only k_rs_tc launch is the one-matrix decode
