@@ -486,7 +486,7 @@ def alg_bytes(k, e, L):
     return {"k_rs_bs(encode)": blk_op, "k_rs_encode_lh": blk_op, "k_dot_generic": blk_op,
             "k_dot_generic(decode)": blk_op, "k_rs_decode_fused": blk_op,
             "k_rs_tc(encode)": blk_op, "k_rs_tc(decode)": blk_op, "k_rs_jit(decode)": blk_op,
-            "k_rs_jit16(decode)": blk_op, "k_rs_jit10(decode)": blk_op, "k_rs_jit(encode)": blk_op,
+            "k_rs_jit16(decode)": blk_op, "k_rs_jit10(decode)": blk_op, "k_rs_jit12(decode)": blk_op, "k_rs_jit(encode)": blk_op,
             "k_decode_prepare": 0.0, "k_decode_prepare_syn": 0.0}
 
 

@@ -158,8 +158,9 @@ size_t rsgpu_decode_workspace_bytes(int k, int e, size_t blocks);
  *   GENERATED   the ONE_MATRIX rows baked into per-block straight-line code
  *               (written to executable device memory by the prepare step),
  *               one call per chunk of sources: 2 waves x 16 rows for
- *               24 < e <= 32 (k_rs_jit16), 2 waves x 10 rows for
- *               16 < e <= 20 (k_rs_jit10), else waves of 8 rows in passes
+ *               24 < e <= 32 (k_rs_jit16), x 12 rows for 20 < e <= 24
+ *               (k_rs_jit12), x 10 rows for 16 < e <= 20 (k_rs_jit10),
+ *               else waves of 8 rows in passes
  *               of 32 rows (k_rs_jit; e <= 63; AUTO takes it for
  *               32 < e <= 63 too)
  * A choice that does not apply to a geometry falls back to GENERAL (e > 32,

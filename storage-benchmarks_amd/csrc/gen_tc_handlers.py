@@ -250,7 +250,7 @@ def main() -> None:
     lines.append("#define RSGPU_TC_ACC_CLOBBERS " + ", ".join(f'"v{ACC + i}"' for i in range(64)))
     # k_rs_jitw<R> (rs_jit.h Wide): R rows per wave, 8 R accumulators from v40
     A16 = 40
-    for R in (16, 10):
+    for R in (16, 12, 10):
         lines.append(f"#define RSGPU_J{R}_ZERO \\")
         for i in range(0, 8 * R, 2):
             lines.append(f'    "v_mov_b64 v[{A16 + i}:{A16 + i + 1}], 0\\n" \\')

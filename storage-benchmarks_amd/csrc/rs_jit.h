@@ -188,6 +188,9 @@ RJ_HD inline bool code_word(const uint8_t* rows, int k, int nslot, int ch, int o
 //   R = 16 (k_rs_jit16, 24 < e <= 32): 128 accumulators, 168 VGPRs, 3 waves
 //          per SIMD, chunks of 6 sources (6 workgroups per CU); 10 % fewer
 //          VALU instructions, 40 % fewer instruction-cache misses than 4 x 8
+//   R = 12 (k_rs_jit12, 20 < e <= 24): 96 accumulators, 136 VGPRs, 3 waves
+//          per SIMD, chunks of 6 sources; composites twice per source and
+//          tile instead of three times (8 + 8 + 8 rows)
 //   R = 10 (k_rs_jit10, 16 < e <= 20): 80 accumulators, 120 VGPRs, 4 waves
 //          per SIMD, chunks of 5 sources (8 workgroups per CU); composites
 //          twice per source and tile instead of three times (8 + 8 + 4 rows)
@@ -277,6 +280,7 @@ struct Wide {
     }
 };
 using J16 = Wide<16, 6>;
+using J12 = Wide<12, 6>;
 using J10 = Wide<10, 5>;
 
 }  // namespace jit

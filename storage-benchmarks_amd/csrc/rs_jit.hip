@@ -309,6 +309,8 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_num_vgpr(40))) void k_rs
     };
     if constexpr (R == 16)
         asm volatile(RSGPU_J16_ZERO ::: RSGPU_J16_ACC_CLOBBERS);
+    else if constexpr (R == 12)
+        asm volatile(RSGPU_J12_ZERO ::: RSGPU_J12_ACC_CLOBBERS);
     else
         asm volatile(RSGPU_J10_ZERO ::: RSGPU_J10_ACC_CLOBBERS);
     issue(0);
@@ -336,6 +338,11 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_num_vgpr(40))) void k_rs
                          :
                          : [fn] "s"(fn), "{v9}"(la)
                          : RSGPU_JW_CALL_CLOBBERS, "s82", "s83", "scc", "memory", RSGPU_J16_ACC_CLOBBERS);
+        else if constexpr (R == 12)
+            asm volatile("s_swappc_b64 s[82:83], %[fn]"
+                         :
+                         : [fn] "s"(fn), "{v9}"(la)
+                         : RSGPU_JW_CALL_CLOBBERS, "s82", "s83", "scc", "memory", RSGPU_J12_ACC_CLOBBERS);
         else
             asm volatile("s_swappc_b64 s[82:83], %[fn]"
                          :
@@ -472,16 +479,18 @@ __global__ __launch_bounds__(256) void k_jitw_emit(int k, int e, const uint8_t* 
 }
 
 // rows per wave of the 2-wave layout for e rows, 0 = the 8-row layout
-int jitw_rows(int e) { return e > 24 && e <= 32 ? 16 : e > 16 && e <= 20 ? 10 : 0; }
+int jitw_rows(int e) { return e > 24 && e <= 32 ? 16 : e > 20 && e <= 24 ? 12 : e > 16 && e <= 20 ? 10 : 0; }
 
 size_t jitw_chunk_stride(int e)
 {
-    return jitw_rows(e) == 16 ? jit::J16::chunk_stride() : jit::J10::chunk_stride();
+    const int r = jitw_rows(e);
+    return r == 16 ? jit::J16::chunk_stride() : r == 12 ? jit::J12::chunk_stride() : jit::J10::chunk_stride();
 }
 
 size_t jitw_code_bytes(int k, int e, long long blocks)
 {
-    const int cs = jitw_rows(e) == 16 ? jit::J16::CS : jit::J10::CS;
+    const int r = jitw_rows(e);
+    const int cs = r == 16 ? jit::J16::CS : r == 12 ? jit::J12::CS : jit::J10::CS;
     return (size_t)blocks * 2 * ((k + cs - 1) / cs) * jitw_chunk_stride(e);
 }
 
@@ -492,6 +501,9 @@ hipError_t launch_jitw_emit(int k, int e, long long blocks, const uint8_t* coef,
         return hipErrorInvalidValue;
     if (jitw_rows(e) == 16)
         hipLaunchKernelGGL(k_jitw_emit<jit::J16>, dim3(2, (unsigned)blocks), dim3(256), 0, st, k, e, coef, status,
+                           code);
+    else if (jitw_rows(e) == 12)
+        hipLaunchKernelGGL(k_jitw_emit<jit::J12>, dim3(2, (unsigned)blocks), dim3(256), 0, st, k, e, coef, status,
                            code);
     else
         hipLaunchKernelGGL(k_jitw_emit<jit::J10>, dim3(2, (unsigned)blocks), dim3(256), 0, st, k, e, coef, status,
@@ -506,6 +518,8 @@ hipError_t launch_rs_jitw(const JitArgs& a, long long blocks, hipStream_t st)
     dim3 grid((unsigned)((a.len + 2047) / 2048), (unsigned)blocks);
     if (jitw_rows(a.rows) == 16)
         hipLaunchKernelGGL(jitk::k_rs_jitw<jit::J16>, grid, dim3(128), 0, st, a);
+    else if (jitw_rows(a.rows) == 12)
+        hipLaunchKernelGGL(jitk::k_rs_jitw<jit::J12>, grid, dim3(128), 0, st, a);
     else
         hipLaunchKernelGGL(jitk::k_rs_jitw<jit::J10>, grid, dim3(128), 0, st, a);
     return hipGetLastError();

@@ -1044,8 +1044,8 @@ WsLayout ws_layout(int k, int e, size_t blocks)
     return w;
 }
 
-// Generated decode code of a call: two waves of 16 rows for 24 < e <= 32 or
-// of 10 rows for 16 < e <= 20 (rs_jit.h Wide: the composites of a source
+// Generated decode code of a call: two waves of 16 rows for 24 < e <= 32, of
+// 12 for 20 < e <= 24, of 10 for 16 < e <= 20 (rs_jit.h Wide: the composites of a source
 // built twice per tile instead of 4 or 3 times), else waves of 8 rows in
 // passes of 32.  k_rs_jit16 measured on the same boxes (tools/jit16_ab.hip,
 // profiles/r02_ab/jit_rows16): 10 % fewer VALU instructions, 40 % fewer
@@ -1061,7 +1061,8 @@ size_t decode_code_bytes(int k, int e, size_t blocks)
 int emit_decode_code(rsgpu_ctx* ctx, int k, int e, size_t blocks, const uint8_t* coef, const int* d_status)
 {
     if (jitw_rows(e)) {
-        KTimer ke(ctx, jitw_rows(e) == 16 ? "k_jit16_emit" : "k_jit10_emit", blocks);
+        KTimer ke(ctx, jitw_rows(e) == 16 ? "k_jit16_emit" : jitw_rows(e) == 12 ? "k_jit12_emit" : "k_jit10_emit",
+                  blocks);
         RS_HIP(ctx, launch_jitw_emit(k, e, (long long)blocks, coef, d_status, (uint8_t*)ctx->d_jit, ctx->stream));
     } else {
         KTimer ke(ctx, "k_jit_emit", blocks);
@@ -1096,7 +1097,11 @@ int jit_decode_launch(rsgpu_ctx* ctx, int k, int e, size_t len, size_t blocks,
         // 16-row kernel (23.3 vs 24.2 ms, profiles/r02_ab/jit_rows16/xcd_*.log),
         // where the 8-row kernel measured 1 % slower
         j.xcd_order = 1;
-        KTimer kt(ctx, jitw_rows(e) == 16 ? "k_rs_jit16(decode)" : "k_rs_jit10(decode)", blocks);
+        KTimer kt(ctx,
+                  jitw_rows(e) == 16   ? "k_rs_jit16(decode)"
+                  : jitw_rows(e) == 12 ? "k_rs_jit12(decode)"
+                                       : "k_rs_jit10(decode)",
+                  blocks);
         RS_HIP(ctx, launch_rs_jitw(j, (long long)blocks, ctx->stream));
         return RSGPU_OK;
     }
@@ -1500,6 +1505,8 @@ long long rsgpu_internal_jitw_emit(int k, int e, const unsigned char* coef, unsi
         o64[i] = (uint64_t)jit::S_NOP0 << 32 | jit::S_SETPC_82;
     if (jitw_rows(e) == 16)
         jitw_emit_host<jit::J16>(k, e, coef, o64);
+    else if (jitw_rows(e) == 12)
+        jitw_emit_host<jit::J12>(k, e, coef, o64);
     else
         jitw_emit_host<jit::J10>(k, e, coef, o64);
     return (long long)need;

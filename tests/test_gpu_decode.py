@@ -90,7 +90,9 @@ GEOMS = [(16, 4, 1000000, 2), (64, 32, 1000000, 2), (100, 20, 1000000, 2), (16, 
          # 24 < e <= 32: 16 rows per wave (k_rs_jit16) when generated;
          # 16 < e <= 20: 10 rows per wave (k_rs_jit10)
          (50, 25, 98304, 3), (31, 31, 4096, 2), (218, 32, 2048, 2),
-         (17, 17, 65536, 2), (64, 19, 4096, 3), (230, 20, 2048, 2)]
+         (17, 17, 65536, 2), (64, 19, 4096, 3), (230, 20, 2048, 2),
+         # 20 < e <= 24: 12 rows per wave (k_rs_jit12)
+         (48, 24, 65536, 2), (21, 21, 4096, 3), (226, 24, 2048, 2)]
 
 
 @pytest.mark.parametrize("kernel", KERNELS)

@@ -254,11 +254,11 @@ def emitw(k, e, coef):
 
 
 # Wide<R, CS>::chunk_stride(): (CS * (112 + 64 R) + 8) rounded to 64
-WIDE = {16: (6, 6848), 10: (5, 3776)}
+WIDE = {16: (6, 6848), 12: (6, 5312), 10: (5, 3776)}
 
 
 @pytest.mark.parametrize("k,e", [(64, 32), (25, 25), (100, 30), (13, 27), (218, 32),
-                                 (100, 20), (17, 17), (64, 19), (230, 20)])
+                                 (100, 20), (17, 17), (64, 19), (230, 20), (48, 24), (21, 21), (226, 24)])
 def test_generated_wide_block_decodes(k, e):
     """k_rs_jitw's code (rs_jit.h Wide: 2 waves x R rows, R = 16 for
     24 < e <= 32 and 10 for 16 < e <= 20, chunks of CS sources, each source
@@ -266,7 +266,7 @@ def test_generated_wide_block_decodes(k, e):
     sum_q c[row][q] * src_q over GF(2^8), only the allowed instructions
     appear, every register is read after its LDS load was waited for, and
     each chunk returns right after its last source."""
-    R = 16 if e > 24 else 10
+    R = 16 if e > 24 else 12 if e > 20 else 10
     cs, stride = WIDE[R]
     rng = random.Random(k * 7 + e)
     coef = np.array([[rng.randrange(256) for _ in range(k)] for _ in range(e)], np.uint8)

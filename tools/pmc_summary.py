@@ -8,7 +8,7 @@ from collections import defaultdict
 
 def short(k: str) -> str:
     if "k_rs_jitw" in k:  # rs_jit.h Wide<R, CS>
-        return "k_rs_jit16(decode)" if "Wide<16" in k else "k_rs_jit10(decode)"
+        return "k_rs_jit%s(decode)" % ("16" if "Wide<16" in k else "12" if "Wide<12" in k else "10")
     if "k_rs_jit" in k:  # <NW, true>: the shared-program encode
         return "k_rs_jit(encode)" if "true>" in k.split("(")[0] else "k_rs_jit(decode)"
     for key in ("k_rs_decode_fused", "k_rs_tc", "k_rs_jit", "k_rs_bs", "k_dot_generic",

@@ -19,7 +19,7 @@ def name_of(kernel: str) -> str:
     if "k_rs_decode_fused" in kernel:
         return "k_rs_decode_fused"
     if "k_rs_jitw" in kernel:  # rs_jit.h Wide<R, CS>
-        return "k_rs_jit16(decode)" if "Wide<16" in kernel else "k_rs_jit10(decode)"
+        return "k_rs_jit%s(decode)" % ("16" if "Wide<16" in kernel else "12" if "Wide<12" in kernel else "10")
     if "k_rs_jit" in kernel:
         return "k_rs_jit(encode)" if "true>" in kernel.split("(")[0] else "k_rs_jit(decode)"
     if "k_rs_tc" in kernel:  # the bench's only k_rs_tc launch is the one-matrix decode
