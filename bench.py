@@ -69,7 +69,7 @@ def parse(argv=None):
     p.add_argument("--loss-rate", type=float, default=None, help="override the config's loss_rate")
     p.add_argument("--seed", type=int, default=1)
     p.add_argument("--decode-kernel", default="auto",
-                   choices=["auto", "generated", "one_matrix", "fused", "general"])
+                   choices=["auto", "generated", "one_matrix", "general"])
     p.add_argument("--encode-kernel", default="auto",
                    choices=["auto", "compiled", "generated", "threaded"])
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -96,6 +96,14 @@ def shard(rank: int, blocks_per_rank: int):
     """Blocks owned by `rank`: [rank*B, (rank+1)*B) -- independent blocks, no
     exchange between ranks; weak scaling."""
     return rank * blocks_per_rank, blocks_per_rank
+
+
+def split(total: int, rank: int, world: int):
+    """A total of `total` blocks over `world` ranks (C4's 2^20): contiguous
+    shares, the first total % world ranks one block more, so every block is
+    owned by exactly one rank.  Returns (first block, blocks) of `rank`."""
+    base, rem = divmod(total, world)
+    return rank * base + min(rank, rem), base + (1 if rank < rem else 0)
 
 
 def reduce_max_time(elapsed: float, world: int, device) -> float:
@@ -235,88 +243,52 @@ def host_io_rate(rsgpu, ctx, k, e, L, blocks, seed, reps=3):
             "verified": ok, "poisoned": True}
 
 
-def host_io_pipelined(rsgpu, ctx, k, e, L, blocks, seed, chunk=4, reps=3):
-    """The host_io_rate workload with the copies overlapped: the blocks go in
-    chunks of `chunk` blocks through three streams (H2D, compute, D2H) joined
-    by events, so chunk i+1 crosses PCIe while chunk i is encoded or decoded
-    and chunk i-1 comes back.  H2D and D2H use the two directions of the link
-    at once.  The decoder side ships only what isa_decoder reads: the k - e
-    surviving source rows (as runs of consecutive rows) and the parity rows;
-    the erased rows hold 0xA5 on the device during the decode leg.  Median
-    of reps."""
+def host_io_pipelined(rsgpu, ctx, k, e, L, blocks, seed, reps=3):
+    """The host_io_rate workload through the library's host-resident calls
+    (rsgpu_encode_blocks_host / rsgpu_decode_blocks_host, the gpu_plugin's
+    --resident host path): blocks in pinned host memory at the reference's
+    pitch of exactly L bytes, streamed through device staging in chunks with
+    copy-in, kernel and copy-out of consecutive chunks overlapped on three
+    streams (both link directions at once).  The decoder ships only what
+    isa_decoder reads (survivor runs + parity); the erased rows hold 0xA5 in
+    host memory during the decode.  Median of reps."""
+    import numpy as np
     import torch
     enc = rsgpu.GpuEncoder(k, L, e, blocks=blocks, seed=seed, ctx=ctx)
     dec = rsgpu.GpuDecoder(k, L, e, blocks=blocks, seed=seed, ctx=ctx)
-    nch = (blocks + chunk - 1) // chunk
-    rk, re_ = k * enc.pitch, e * enc.pitch
-    h_src = torch.empty(enc.src.numel(), dtype=torch.uint8, pin_memory=True)
-    h_par = torch.empty(enc.par.numel(), dtype=torch.uint8, pin_memory=True)
-    h_out = torch.empty(dec.out.numel(), dtype=torch.uint8, pin_memory=True)
-    h_src.copy_(enc.src)
+    h_src = torch.empty((blocks, k, L), dtype=torch.uint8, pin_memory=True)
+    h_par = torch.empty((blocks, e, L), dtype=torch.uint8, pin_memory=True)
+    h_out = torch.empty((blocks, e, L), dtype=torch.uint8, pin_memory=True)
+    h_src.copy_(enc.src.view(blocks, k, enc.pitch)[:, :, :L])
+    keep = h_src.clone()
+    err = np.ascontiguousarray(dec.err_host)
+    st = np.full(blocks, -1, np.int32)
     torch.cuda.synchronize()
-    # one decode workspace per chunk: the chunks' decodes may overlap their copies
-    wss = [torch.empty(rsgpu.decode_workspace_bytes(k, e, chunk), dtype=torch.uint8,
-                       device=enc.src.device) for _ in range(nch)]
-    # decoder side ships only the survivors (found untimed)
-    runs = survivor_runs(dec.err_host, k, enc.pitch, chunk)
-    s_in, s_cmp, s_out = torch.cuda.Stream(), torch.cuda.Stream(), torch.cuda.Stream()
-    prev_stream = ctx.get_stream()
-    ctx.set_stream(s_cmp.cuda_stream)
-
-    def run(decode):
-        for i in range(nch):
-            b0, nb = i * chunk, min(chunk, blocks - i * chunk)
-            src = enc.src[b0 * rk:(b0 + nb) * rk]
-            par = enc.par[b0 * re_:(b0 + nb) * re_]
-            out = dec.out[b0 * re_:(b0 + nb) * re_]
-            e_in, e_cmp = torch.cuda.Event(), torch.cuda.Event()
-            with torch.cuda.stream(s_in):
-                if decode:
-                    for off, n in runs[i]:
-                        enc.src[off:off + n].copy_(h_src[off:off + n], non_blocking=True)
-                    par.copy_(h_par[b0 * re_:(b0 + nb) * re_], non_blocking=True)
-                else:
-                    src.copy_(h_src[b0 * rk:(b0 + nb) * rk], non_blocking=True)
-                e_in.record(s_in)
-            s_cmp.wait_event(e_in)
-            if decode:
-                ctx.decode_blocks(k, e, L, enc.pitch, nb, src, par, dec.err[b0:b0 + nb], out,
-                                  wss[i], dec.status[b0:b0 + nb])
-            else:
-                ctx.encode_blocks(k, e, L, enc.pitch, nb, src, par)
-            e_cmp.record(s_cmp)
-            s_out.wait_event(e_cmp)
-            with torch.cuda.stream(s_out):
-                if decode:
-                    h_out[b0 * re_:(b0 + nb) * re_].copy_(out, non_blocking=True)
-                else:
-                    h_par[b0 * re_:(b0 + nb) * re_].copy_(par, non_blocking=True)
-        torch.cuda.synchronize()
-
     times = []
-    try:
-        for _ in range(reps):
-            t0 = time.perf_counter()
-            run(False)
-            t1 = time.perf_counter()
-            poison_erased(enc, dec)  # untimed
-            torch.cuda.synchronize()
-            t2 = time.perf_counter()
-            run(True)
-            t3 = time.perf_counter()
-            times.append((t1 - t0, t3 - t2))
-    finally:
-        ctx.set_stream(prev_stream)
-    dec._decoded = True
+    for _ in range(reps):
+        h_src.copy_(keep)
+        t0 = time.perf_counter()
+        ctx.encode_blocks_host(k, e, L, L, blocks, h_src, h_par)
+        t1 = time.perf_counter()
+        for b in range(blocks):  # untimed: what the decoder may not read
+            h_src[b, torch.from_numpy(err[b].astype(np.int64))] = 0xA5
+        t2 = time.perf_counter()
+        ctx.decode_blocks_host(k, e, L, L, blocks, h_src, h_par, err, h_out, st)
+        t3 = time.perf_counter()
+        times.append((t1 - t0, t3 - t2))
     times.sort(key=lambda x: x[0] + x[1])
     te, td = times[len(times) // 2]
-    enc.src.copy_(h_src)  # the originals back for verify_data
+    ok = bool((st == 0).all())
+    for b in range(blocks):
+        idx = torch.from_numpy(err[b].astype(np.int64))
+        ok = ok and bool(torch.equal(h_out[b], keep[b, idx]))
+    # the parity that came back is the device path's
+    enc.encode_all()
     torch.cuda.synchronize()
-    ok = dec.is_complete() and dec.verify_data(enc)
-    # what came back to the host is what the device holds
-    ok = ok and bool(torch.equal(h_out, dec.out.cpu())) and bool(torch.equal(h_par, enc.par.cpu()))
+    ok = ok and bool(torch.equal(h_par, enc.par.view(blocks, e, enc.pitch)[:, :, :L].cpu()))
     out_b = e * L * blocks
-    return {"blocks": blocks, "chunk_blocks": chunk, "encode_s": te, "decode_s": td,
+    return {"blocks": blocks, "path": "rsgpu_encode_blocks_host / rsgpu_decode_blocks_host",
+            "encode_s": te, "decode_s": td,
             "goodput_GiBps": 2 * out_b / (te + td) / 2 ** 30,
             "encode_GiBps": out_b / te / 2 ** 30, "decode_GiBps": out_b / td / 2 ** 30,
             "verified": ok, "poisoned": True}
@@ -484,7 +456,7 @@ def alg_bytes(k, e, L):
     (k + e) L for an encode or a decode (read k rows, write e)."""
     blk_op = float((k + e) * L)
     return {"k_rs_bs(encode)": blk_op, "k_rs_encode_lh": blk_op, "k_dot_generic": blk_op,
-            "k_dot_generic(decode)": blk_op, "k_rs_decode_fused": blk_op,
+            "k_dot_generic(decode)": blk_op,
             "k_rs_tc(encode)": blk_op, "k_rs_tc(decode)": blk_op, "k_rs_jit(decode)": blk_op,
             "k_rs_jit16(decode)": blk_op, "k_rs_jit10(decode)": blk_op, "k_rs_jit12(decode)": blk_op, "k_rs_jit(encode)": blk_op,
             "k_decode_prepare": 0.0, "k_decode_prepare_syn": 0.0}
@@ -501,9 +473,8 @@ def run_streamed(args, rsgpu, ctx, dev, rank, world, k, e, L, total_blocks):
     seconds, wall seconds, mismatching bytes, batches, kernel records)."""
     import numpy as np
     import torch
-    share = total_blocks // world
-    blk_base = rank * share
-    batch = min(args.batch, share)
+    blk_base, share = split(total_blocks, rank, world)
+    batch = max(1, min(args.batch, share))
     nb_total = (share + batch - 1) // batch
     gen_ctx = rsgpu.Context(dev.index)
     s_cmp, s_gen = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
@@ -625,7 +596,11 @@ def main(argv=None):
             del w_enc, w_dec
         timed, wall, bad, nbatches, batch, recs = run_streamed(args, rsgpu, ctx, dev, rank, world,
                                                                k, e, L, B)
-        share = B // world
+        blk0, share = split(B, rank, world)
+        if world > 1:
+            rank_info = [None] * world
+            dist.all_gather_object(rank_info, {"rank": rank, "device": device_index, "block0": blk0,
+                                               "blocks": share, "batches": nbatches})
         elapsed = reduce_max_time(timed, world, red_dev)
         wall = reduce_max_time(wall, world, red_dev)
         bad_t = torch.tensor([float(bad)], dtype=torch.float64, device=red_dev)
@@ -633,15 +608,17 @@ def main(argv=None):
             dist.all_reduce(bad_t)
         ok = args.no_verify or bad_t.item() == 0
         steps = 1
-        out_bytes_step = 2.0 * e * L * share
+        # every rank's share counts (shares differ by at most one block)
+        out_bytes_step = 2.0 * e * L * B / world
         value = job_goodput(out_bytes_step, 1, world, elapsed)
         ms_step = elapsed * 1e3
         workload = (f"isa_throughput c4: symbols={k} symbol_size={L} loss_rate={loss} erased={e} "
-                    f"blocks={B} streamed over {world} GPU(s): {share} per GPU in {nbatches} "
+                    f"blocks={B} streamed over {world} GPU(s): {share} on rank {rank} in {nbatches} "
                     f"batches of {batch} (2 resident)")
-        extra = {"streamed": {"blocks_total": B, "blocks_per_gpu": share, "batches": nbatches,
+        extra = {"streamed": {"blocks_total": B, "blocks_per_gpu": B / world, "blocks_rank0": share,
+                              "batches": nbatches,
                               "batch_blocks": batch, "timed_s": elapsed, "wall_s": wall,
-                              "wall_GiBps": 2.0 * e * L * share * world / wall / 2 ** 30,
+                              "wall_GiBps": 2.0 * e * L * B / wall / 2 ** 30,
                               "mismatch_bytes": bad_t.item(),
                               "note": "value: encode+decode regions (HIP events) summed over "
                                       "the batches; wall: the whole stream incl. on-device "

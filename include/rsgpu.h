@@ -151,8 +151,6 @@ size_t rsgpu_decode_workspace_bytes(int k, int e, size_t blocks);
  *               pairs, else ONE_MATRIX (the default)
  *   ONE_MATRIX  closed-form e x k decode rows V_E^-1 [V_kept | I] (e <= 32),
  *               one threaded-code pass over the k - e survivors + e parity
- *   FUSED       syndromes and the e x e solve per column tile in one kernel
- *               (e <= 32, k <= 128)
  *   GENERAL     the reference's k x k survivor-matrix inversion on the
  *               device (isa.cpp:177-204), then the decode rows; any e
  *   GENERATED   the ONE_MATRIX rows baked into per-block straight-line code
@@ -167,7 +165,7 @@ size_t rsgpu_decode_workspace_bytes(int k, int e, size_t blocks);
  * unaligned rows) or ONE_MATRIX. */
 #define RSGPU_DECODE_AUTO 0
 #define RSGPU_DECODE_ONE_MATRIX 1
-#define RSGPU_DECODE_FUSED 2
+/* 2 is retired (a fused syndrome + solve kernel, never faster; removed) */
 #define RSGPU_DECODE_GENERAL 3
 #define RSGPU_DECODE_GENERATED 4
 int rsgpu_set_decode_kernel(rsgpu_ctx *ctx, int kernel);
@@ -193,13 +191,14 @@ int rsgpu_decode_blocks(rsgpu_ctx *ctx, int k, int e, size_t len, size_t pitch, 
  * prepare = survivor matrix + gf_invert_matrix + decode tables + row pointers
  * (isa.cpp:177-207) into d_workspace and d_status; apply = the dot product
  * (isa.cpp:208-209) for blocks whose status is 0.  decode_blocks ==
- * prepare followed by apply on the same stream.  apply may fan work out to an
- * internal second stream; it always joins back, so everything it wrote is
- * ordered before later work on the context stream.  At most 65535 blocks
- * per call (RSGPU_ERR_ARG beyond).  apply must be given the geometry, block
+ * prepare followed by apply on the same stream.  At most 65535 blocks per
+ * call (RSGPU_ERR_ARG beyond).  apply must be given the geometry, block
  * count, buffers and workspace of the prepare before it, with no
  * rsgpu_set_decode_kernel in between: both derive the decode kernel (and so
- * the workspace layout) from them. */
+ * the workspace layout) from them.  The generated-code decode keeps the code
+ * of the context's LAST prepare: an apply whose (k, e, blocks, workspace)
+ * differ from it, or that follows another decode call on the context (which
+ * rewrites or regrows the code), returns RSGPU_ERR_ARG and launches nothing. */
 int rsgpu_decode_prepare(rsgpu_ctx *ctx, int k, int e, size_t len, size_t pitch, size_t blocks,
                          const unsigned char *d_src, const unsigned char *d_parity,
                          const unsigned char *d_err, unsigned char *d_out, void *d_workspace,
@@ -233,6 +232,36 @@ int rsgpu_decode_general(rsgpu_ctx *ctx, int k, int m, size_t len, size_t pitch,
 int rsgpu_verify_blocks(rsgpu_ctx *ctx, int k, int e, size_t len, size_t pitch, size_t blocks,
                         const unsigned char *d_src, const unsigned char *d_out,
                         const unsigned char *d_err, unsigned long long *d_mismatch);
+
+/* ---- host-resident blocks (the reference's buffers, isa.cpp:46-58) ------- */
+
+/* Page-locked host memory for the host-resident calls: their copies then run
+ * as DMA at the link rate and overlap the kernels (pageable memory works,
+ * but is copied synchronously, so the stages run in series). */
+int rsgpu_host_alloc(rsgpu_ctx *ctx, void **hptr, size_t bytes);
+int rsgpu_host_free(rsgpu_ctx *ctx, void *hptr);
+
+/* isa_encoder::encode_all over blocks held in HOST memory, as isa.cpp:46-58
+ * holds them (isa.cpp:69-79): h_src [blocks][k] rows, h_parity [blocks][e]
+ * rows, at `pitch` >= len.  The batch streams through device staging in
+ * chunks, copy-in / rsgpu_encode_blocks / copy-out of consecutive chunks
+ * overlapped on three streams.  Synchronous: the parity is in h_parity on
+ * return.  `coef` as rsgpu_encode_blocks. */
+int rsgpu_encode_blocks_host(rsgpu_ctx *ctx, int k, int e, size_t len, size_t pitch, size_t blocks,
+                             const unsigned char *h_src, unsigned char *h_parity,
+                             const unsigned char *coef);
+
+/* isa_decoder::decode_all over HOST-resident blocks (isa.cpp:169-213): the
+ * erasure lists h_err [blocks][e] as rsgpu_decode_blocks; only what the
+ * reference's decoder reads crosses the link towards the GPU -- the surviving
+ * originals (as runs of consecutive rows; rows shorter than 64 KiB go as
+ * whole blocks, erased rows included, which the kernels never read) and the
+ * parity rows -- and the recovered rows land in h_out [blocks][e] (in h_err
+ * order).  h_status [blocks] (may be NULL) receives rsgpu_decode_blocks'
+ * per-block status.  Pipelined and synchronous as rsgpu_encode_blocks_host. */
+int rsgpu_decode_blocks_host(rsgpu_ctx *ctx, int k, int e, size_t len, size_t pitch, size_t blocks,
+                             const unsigned char *h_src, const unsigned char *h_parity,
+                             const unsigned char *h_err, unsigned char *h_out, int *h_status);
 
 /* ---- synthetic workload (replaces rand(), isa.cpp:56-58, :137-146) ------- */
 

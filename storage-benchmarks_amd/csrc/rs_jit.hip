@@ -40,34 +40,22 @@ using bs::wait_vm;
 
 constexpr int C = 8;  // sources per LDS chunk (double-buffered)
 
-// Phase accounting for tools/jit_profile.hip (compiled in only there, with
-// -DRSGPU_JIT_PROF): per-wave s_memtime sums of each phase, sampled
-// workgroups, added into rsgpu_jit_prof[phase] at the end of the wave.
-#ifdef RSGPU_JIT_PROF
-__device__ unsigned long long rsgpu_jit_prof[8];
-#define JP_DECL unsigned long long jp_sum[8] = {}, jp_t = __builtin_amdgcn_s_memtime(), jp_start = jp_t;
-#define JP_MARK(P)                                                     \
-    do {                                                               \
-        const unsigned long long jp_n = __builtin_amdgcn_s_memtime();  \
-        jp_sum[P] += jp_n - jp_t;                                      \
-        jp_t = jp_n;                                                   \
-    } while (0)
-#define JP_END                                                                          \
-    do {                                                                                \
-        jp_sum[7] = __builtin_amdgcn_s_memtime() - jp_start;                            \
-        if (lane == 0 && (blockIdx.x & 63) == 0)                                        \
-            for (int i = 0; i < 8; ++i)                                                 \
-                atomicAdd(&rsgpu_jit_prof[i], jp_sum[i]);                               \
-    } while (0)
-#else
-#define JP_DECL
-#define JP_MARK(P) \
-    do {           \
-    } while (0)
-#define JP_END \
-    do {       \
-    } while (0)
-#endif
+// Instrumentation points of k_rs_jit.  The product instantiates JitHooks:
+// no timers, every wave runs its own block's code, wave 0 invalidates the
+// instruction cache.  tools/jit_profile.hip supplies its own policy (per-phase
+// s_memtime sums, timing-only code substitution) without touching this file.
+struct JitHooks {
+    struct Timer {
+        __device__ void mark(int) {}
+        __device__ void end(int) {}
+    };
+    static constexpr bool kInvalidate = true;
+    // this wave's generated code: chunk ch at code + ch * chunk_stride
+    __device__ static const uint8_t* code(const JitArgs& a, bool shared, int b, int wave, int nch)
+    {
+        return a.code + (shared ? 0 : (size_t)b * a.block_stride) + (size_t)wave * nch * a.chunk_stride;
+    }
+};
 
 template <int S>
 __device__ __forceinline__ void read_slot(uint32_t (&W)[8])
@@ -97,7 +85,7 @@ __device__ __forceinline__ void read_slot(uint32_t (&W)[8])
 // 26.3 vs 25.1 ms at C3, tools/jit_profile.)
 // SH: one program shared by every block (the GENERATED encode; a distinct
 // symbol, so profiles tell it from the per-block decode)
-template <int NW, bool SH>
+template <int NW, bool SH, class H = JitHooks>
 __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_num_vgpr(64))) void k_rs_jit(JitArgs a)
 {
     __shared__ uint4 lds[2][C * 2 * 64];
@@ -121,12 +109,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_num_vgpr(64))) void 
     const int nch = (k + C - 1) / C;
     const uint8_t* const* srcs = a.srcs + (size_t)b * k;
     uint8_t* const* dsts = a.dsts + (size_t)b * a.dst_stride;
-    // this wave's generated code: chunk ch at code + ch * stride
-#ifndef RSGPU_JIT_SHARE
-    const uint8_t* code = a.code + (SH ? 0 : (size_t)b * a.block_stride) + (size_t)wave * nch * a.chunk_stride;
-#else  // timing-only builds of tools/jit_profile: 1 = every wave runs wave 0's code, 2 = block 0's too
-    const uint8_t* code = a.code + (size_t)(RSGPU_JIT_SHARE == 2 ? 0 : b) * a.block_stride;
-#endif
+    const uint8_t* code = H::code(a, SH, b, wave, nch);
     const uint32_t m4 = vconst(0x0F0F0F0Fu), m2 = vconst(0x33333333u), m1 = vconst(0x55555555u);
     const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint4*)&lds[0][0];
     const long long off = tile * 2048 + lane * 32;
@@ -137,10 +120,8 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_num_vgpr(64))) void 
     // workgroup calls code (the calls follow the first chunk barrier).  Every
     // wave invalidating measured 1.3 % slower (it wipes the other workgroups'
     // lines too; profiles/r02_ab/jit_icache_inv.log).
-#ifndef RSGPU_JIT_NO_INV  // timing-only builds: code unchanged between launches
-    if (wave == 0)
+    if (H::kInvalidate && wave == 0)
         asm volatile("s_icache_inv\n s_nop 15\n s_nop 15" ::: "memory");
-#endif
 
     // chunk ch's sources this wave moves: t = wave, wave + NW, ... (two row
     // pointers per scalar wait)
@@ -162,14 +143,14 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_num_vgpr(64))) void 
     };
 
     asm volatile(RSGPU_TC_ZERO ::: RSGPU_TC_ACC_CLOBBERS);
-    JP_DECL
+    typename H::Timer jp;
     issue(0);
-    JP_MARK(3);
+    jp.mark(3);
     for (int ch = 0; ch < nch; ++ch) {
         const int nt = min(C, k - ch * C);
         uint4* buf = lds[ch & 1];
         wait_vm(0);  // this chunk's own sources, issued behind the previous barrier
-        JP_MARK(0);
+        jp.mark(0);
         // own share of this chunk: bytes -> bit-planes, in place, two
         // sources at a time (both sets of LDS reads in flight together)
         int t = wave;
@@ -194,14 +175,14 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_num_vgpr(64))) void 
             buf[(t * 2 + 0) * 64 + lane] = make_uint4(W[0], W[1], W[2], W[3]);
             buf[(t * 2 + 1) * 64 + lane] = make_uint4(W[4], W[5], W[6], W[7]);
         }
-        JP_MARK(1);
+        jp.mark(1);
         barrier_lds();
-        JP_MARK(2);
+        jp.mark(2);
         // one barrier per chunk: every wave is past its call of chunk ch - 1,
         // which read buffer (ch + 1) & 1, so chunk ch + 1 may land there now
         if (ch + 1 < nch)
             issue(ch + 1);
-        JP_MARK(3);
+        jp.mark(3);
         const uint32_t la = lds0 + (uint32_t)((ch & 1) * C * 2 * 64 * 16) + lane * 16;
         const uint8_t* fn = code + (size_t)ch * a.chunk_stride;
         asm volatile("s_swappc_b64 s[82:83], %[fn]"
@@ -212,7 +193,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_num_vgpr(64))) void 
                        "v46", "v47", "v48", "v49", "v50", "v51", "v52", "v53", "v54", "v55", "v56",
                        "v57", "v58", "v59", "v60", "v61", "s82", "s83", "scc", "memory",
                        RSGPU_TC_ACC_CLOBBERS);
-        JP_MARK(4);
+        jp.mark(4);
     }
     // outputs back to bytes and out (every source of this tile was read
     // before the last barrier)
@@ -231,8 +212,8 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_num_vgpr(64))) void 
                 ...);
         }(std::make_integer_sequence<int, 8>{});
     }
-    JP_MARK(5);
-    JP_END;
+    jp.mark(5);
+    jp.end(lane);
 }
 
 template <int S>

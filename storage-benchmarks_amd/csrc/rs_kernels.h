@@ -68,31 +68,20 @@ bool rs_bitsliced_available(int k, int e);
 hipError_t launch_rs_bitsliced(int k, int e, const uint8_t* src, uint8_t* out, long long pitch,
                                long long len, long long blocks, hipStream_t st);
 
-// Syndrome-form decode prepare for the gf_gen_rs_matrix code with e erased
-// originals and all e parity rows surviving (e <= 32), per block: erasure
-// list validation (strictly ascending, < k; else status -2), emask [B][2],
-// and one of
-//   dir_addr != nullptr  the one-matrix decode through k_rs_tc: srcs [B][k]
-//                        = surviving originals (ascending) then the e parity
-//                        rows, dsts [B][e] = out rows, dir_addr [B][k][slots]
-//                        = handler addresses of the e x k decode rows
-//                        V_E^-1 [V_kept | I] (closed form, no elimination)
-//   otherwise            the fused decode's tables: tc_addr [B][e][slots]
-//                        handler addresses of V_E^-1 (e x e Gauss-Jordan) and
-//                        syn_addr [B][k-e][slots] of the syndrome rows
-//                        2^(r j) per surviving original j (ascending)
-// slots = tc_rows_per_pass(e); tc_table = the context's handler addresses.
-// jit_coef != nullptr (with dir_addr == nullptr, one-matrix form): instead of
-// handler addresses, the e x k decode rows themselves, [B][e][k] bytes, which
-// launch_jit_emit turns into k_rs_jit's code.
+// Closed-form decode prepare for the gf_gen_rs_matrix code with e erased
+// originals and all e parity rows surviving, per block: erasure list
+// validation (strictly ascending, < k; else status -2), srcs [B][k] =
+// surviving originals (ascending) then the e parity rows, dsts [B][e] = out
+// rows, and the e x k decode rows V_E^-1 [V_kept | I] (no elimination) as
+//   dir_addr != nullptr  k_rs_tc handler addresses [B][k][tc_rows_per_pass(e)]
+//                        (e <= 32; tc_table = the context's handler table)
+//   jit_coef != nullptr  the rows themselves, [B][e][k] bytes, which the
+//                        emitters turn into k_rs_jit / k_rs_jitw code (e <= 63)
 hipError_t launch_decode_prepare_syn(int k, int e, long long blocks, const uint8_t* err,
                                      uint8_t* out, long long out_pitch, const uint8_t** srcs,
-                                     uint8_t** dsts, const unsigned long long* tc_table,
-                                     unsigned long long* tc_addr, unsigned long long* emask,
-                                     int* status, unsigned long long* syn_addr,
+                                     uint8_t** dsts, const unsigned long long* tc_table, int* status,
                                      const uint8_t* src, const uint8_t* par,
-                                     unsigned long long* dir_addr, uint8_t* jit_coef,
-                                     hipStream_t st);
+                                     unsigned long long* dir_addr, uint8_t* jit_coef, hipStream_t st);
 
 // The one-matrix decode through generated code (rs_jit.hip).
 struct JitArgs {
@@ -117,7 +106,8 @@ hipError_t launch_jit_emit(int k, int e, long long blocks, const uint8_t* coef, 
 hipError_t launch_jit_fill(void* code, size_t bytes, hipStream_t st);
 hipError_t launch_rs_jit(const JitArgs& a, long long blocks, hipStream_t st);
 // Two waves of R rows per tile (rs_jit.h Wide): R = jitw_rows(e) (16 for
-// 24 < e <= 32, 10 for 16 < e <= 20, else 0 = not this layout); code of
+// 24 < e <= 32, 12 for 20 < e <= 24, 10 for 16 < e <= 20, else 0 = not this
+// layout); code of
 // block b, wave w, chunk ch at code + ((b 2 + w) nch + ch) jitw_chunk_stride(e)
 int jitw_rows(int e);
 size_t jitw_chunk_stride(int e);
@@ -165,16 +155,6 @@ __host__ __device__ inline long long tc_elem(int k, int rows, int r, int j)
     return tc_pass_offset(k, p) + (long long)j * tc_rows_per_pass(tc_pass_rows(rows, p)) + (r & 31);
 }
 
-// One-pass syndrome decode (rs_decode_fused.hip) for the instantiated
-// gf_gen_rs_matrix codes: out[b] = data rows listed by the prepare kernel's
-// emask, from src (surviving data) and par; addr = k_rs_tc handler addresses
-// of V_E^-1 ([B][e][tc_rows_per_pass(e)]); blocks with status != 0 skipped.
-bool rs_decode_fused_available(int k, int e);
-hipError_t launch_rs_decode_fused(int k, int e, const uint8_t* src, const uint8_t* par,
-                                  uint8_t* out, long long pitch, long long len, long long blocks,
-                                  const uint64_t* emask, const unsigned long long* addr,
-                                  const unsigned long long* syn_addr, const int* status,
-                                  hipStream_t st);
 int tc_handler_stride();
 // handlers in the table (256 per handler copy of the chained dispatch) and
 // the copy serving slot s (0..7).  Consumers index the context's 2048-entry

@@ -863,25 +863,25 @@ hipError_t launch_update(const uint8_t* data, uint8_t* const* coding, const uint
 }
 
 // ---------------------------------------------------------------------------
-// Decode preparation, syndrome form (one workgroup per block)
+// Decode preparation, closed form (one workgroup per block)
 // ---------------------------------------------------------------------------
 // With all e parity rows surviving and e erased ORIGINALS E = {j_0 < ... },
 // the survivor matrix b of isa.cpp:177-182 is singular iff the e x e block
-// V_E[p][i] = 2^(p*j_i) is (det b = det V_E up to row order).  The recovered
-// symbols are the unique solution of V_E x = s with the syndromes
-// s_p = P_p ^ sum_{j not in E} 2^(p j) d_j, so the decode needs V_E^-1 only.
-// Outputs: emask[b][2], srcs[b][e] = dsts[b][e] = out rows (the syndrome
-// kernel writes s into out; the dot product then runs in place), tables of
-// V_E^-1 as [p][rows_pad], status.
+// V_E[p][i] = 2^(p*j_i) is (det b = det V_E up to row order), and V_E is
+// Vandermonde in distinct points, so never singular.  The recovered symbols
+// are the unique solution of V_E x = s with the syndromes
+// s_p = P_p ^ sum_{j not in E} 2^(p j) d_j; the decode rows below apply
+// V_E^-1 [V_kept | I] to the survivors and the parity rows in one pass.
+// Outputs: srcs[b][k] (survivors ascending, then the parity rows), dsts[b][e]
+// = out rows, status, and either the k_rs_tc handler addresses dir_addr
+// [b][k][slots] or the decode rows jit_coef [b][e][k] for the emitters.
 __global__ __launch_bounds__(256) void k_decode_prepare_syn(int k, int e,
                                                             const uint8_t* __restrict__ err,
                                                             uint8_t* out, long long out_pitch,
                                                             const uint8_t** srcs, uint8_t** dsts,
                                                             const unsigned long long* tc_table,
-                                                            unsigned long long* tc_addr,
-                                                            unsigned long long* emask, int* status,
-                                                            unsigned long long* syn_addr,
-                                                            const uint8_t* src, const uint8_t* par,
+                                                            int* status, const uint8_t* src,
+                                                            const uint8_t* par,
                                                             unsigned long long* dir_addr,
                                                             uint8_t* jit_coef)
 {
@@ -890,7 +890,6 @@ __global__ __launch_bounds__(256) void k_decode_prepare_syn(int k, int e,
     uint8_t* glog = lds + 512;    // 256
     int* sh = reinterpret_cast<int*>(lds + 768);  // 16 ints
     uint8_t* A = lds + 832;       // e*e
-    uint8_t* Dm = A + e * e;      // e*e
     const int b = blockIdx.x;
     const int tid = threadIdx.x, nt = blockDim.x;
     const uint8_t* eb = err + (size_t)b * e;
@@ -902,18 +901,11 @@ __global__ __launch_bounds__(256) void k_decode_prepare_syn(int k, int e,
     if (tid == 0) {
         // validate: strictly ascending originals
         int bad = 0;
-        unsigned long long m0 = 0, m1 = 0;
         for (int i = 0; i < e; ++i) {
             const int j = eb[i];
             if (j >= k || (i > 0 && j <= eb[i - 1]))
                 bad = 1;
-            else if (j < 64)
-                m0 |= 1ull << j;
-            else if (j < 128)  // the bitmask serves the fused kernel (k <= 128) only
-                m1 |= 1ull << (j - 64);
         }
-        emask[2 * b] = m0;
-        emask[2 * b + 1] = m1;
         sh[0] = bad ? -2 : 0;
     }
     __syncthreads();
@@ -926,7 +918,7 @@ __global__ __launch_bounds__(256) void k_decode_prepare_syn(int k, int e,
         return (x && y) ? gexp[glog[x] + glog[y]] : (uint8_t)0;
     };
     const int tc_rows = tc_rows_per_pass(e);
-    if (dir_addr || jit_coef) {
+    {
         // One-matrix decode through k_rs_tc: sources = the k - e surviving
         // originals (ascending) then the e parity rows, outputs = the erased
         // originals.  d_E = V_E^-1 (P ^ V_kept d_kept), V_E[p][i] = a_i^p with
@@ -939,7 +931,7 @@ __global__ __launch_bounds__(256) void k_decode_prepare_syn(int k, int e,
         //   (V_E^-1)[i][p]          = [z^p] L_i(z) = [z^p] (Lambda(z) / (z + a_i)) / w_i
         //   (V_E^-1 V_kept)[i][q]   = L_i(b_q)     = Lambda(b_q) / ((b_q + a_i) w_i)
         // with b_q = 2^(j_q) for survivor q: O(e k) work, no elimination.
-        uint8_t* lv = Dm + e * e;  // survivors, k - e bytes (256 reserved)
+        uint8_t* lv = A + e * e;   // survivors, k - e bytes (256 reserved)
         uint8_t* lam = lv + 256;   // Lambda coefficients, e + 1 (64 reserved)
         uint8_t* lw = lam + 64;    // log w_i (64 reserved)
         uint8_t* lb = lw + 64;     // log Lambda(b_q) (256 reserved)
@@ -1028,124 +1020,19 @@ __global__ __launch_bounds__(256) void k_decode_prepare_syn(int k, int e,
             const int q = idx / tc_rows, i = idx - q * tc_rows;
             da[idx] = tc_table[(i & 7) * 256 + dcoef(q, i)];
         }
-        return;
-    }
-    for (int idx = tid; idx < e * e; idx += nt) {
-        const int p = idx / e, i = idx - p * e;
-        A[idx] = gexp[(p * (int)eb[i]) % 255];
-        Dm[idx] = (p == i) ? 1 : 0;
-    }
-    __syncthreads();
-    const int n = e;
-    for (int i = 0; i < n; ++i) {
-        if (tid == 0) {
-            int piv = i;
-            if (A[i * n + i] == 0) {
-                piv = -1;
-                for (int j = i + 1; j < n; ++j)
-                    if (A[j * n + i]) {
-                        piv = j;
-                        break;
-                    }
-            }
-            sh[1] = piv;
-        }
-        __syncthreads();
-        const int piv = sh[1];
-        if (piv < 0) {
-            if (tid == 0)
-                sh[0] = -1;
-            break;
-        }
-        if (piv != i) {
-            for (int c = tid; c < n; c += nt) {
-                uint8_t t = A[i * n + c];
-                A[i * n + c] = A[piv * n + c];
-                A[piv * n + c] = t;
-                t = Dm[i * n + c];
-                Dm[i * n + c] = Dm[piv * n + c];
-                Dm[piv * n + c] = t;
-            }
-            __syncthreads();
-        }
-        const uint8_t pinv = gexp[255 - glog[A[i * n + i]]];
-        __syncthreads();
-        for (int c = tid; c < n; c += nt) {
-            A[i * n + c] = gmul(A[i * n + c], pinv);
-            Dm[i * n + c] = gmul(Dm[i * n + c], pinv);
-        }
-        __syncthreads();
-        for (int idx = tid; idx < n * n; idx += nt) {
-            const int r = idx / n, c = idx - r * n;
-            if (r == i || c == i)
-                continue;
-            const uint8_t f = A[r * n + i];
-            A[idx] ^= gmul(f, A[i * n + c]);
-            Dm[idx] ^= gmul(f, Dm[i * n + c]);
-        }
-        __syncthreads();
-        for (int r = tid; r < n; r += nt) {
-            if (r == i)
-                continue;
-            const uint8_t f = A[r * n + i];
-            Dm[r * n + i] ^= gmul(f, Dm[i * n + i]);
-            A[r * n + i] = 0;
-        }
-        __syncthreads();
-    }
-    __syncthreads();
-    const int st = sh[0];
-    if (tid == 0)
-        status[b] = st;
-    if (st != 0)
-        return;
-    {
-        // syndrome phase of the fused decode (threaded code): the q-th
-        // surviving original j_q (ascending) carries coefficient 2^(r j_q)
-        // for syndrome row r = slot (gf_gen_rs_matrix row k + r,
-        // isa/ec_base.c:71-78); [q][slot], padding slots -> handler 0
-        uint8_t* lv = Dm + e * e;  // live list, k - e bytes
-        for (int j = tid; j < k; j += nt) {
-            int below = 0;  // erased originals < j (the list is validated ascending)
-            bool er = false;
-            for (int i = 0; i < e; ++i) {
-                below += eb[i] < j;
-                er |= eb[i] == j;
-            }
-            if (!er)
-                lv[j - below] = (uint8_t)j;
-        }
-        __syncthreads();
-        unsigned long long* sa = syn_addr + (size_t)b * (k - e) * tc_rows;
-        for (int idx = tid; idx < (k - e) * tc_rows; idx += nt) {
-            const int q = idx / tc_rows, r = idx - q * tc_rows;
-            sa[idx] = tc_table[(r & 7) * 256 + (r < e ? gexp[(r * (int)lv[q]) % 255] : 0)];
-        }
-    }
-    {
-        // handler addresses [p][slot]: coefficient (V_E^-1)[slot][p], padding
-        // slots -> handler 0 (no-op)
-        unsigned long long* ta = tc_addr + (size_t)b * e * tc_rows;
-        for (int idx = tid; idx < e * tc_rows; idx += nt) {
-            const int p = idx / tc_rows, i = idx - p * tc_rows;
-            ta[idx] = tc_table[(i & 7) * 256 + (i < e ? Dm[i * n + p] : 0)];
-        }
     }
 }
 
-size_t decode_prepare_syn_lds_bytes(int e) { return 832 + 2 * (size_t)e * e + 256 + 512; }
+size_t decode_prepare_syn_lds_bytes(int e) { return 832 + (size_t)e * e + 256 + 512; }
 
 hipError_t launch_decode_prepare_syn(int k, int e, long long blocks, const uint8_t* err,
                                      uint8_t* out, long long out_pitch, const uint8_t** srcs,
-                                     uint8_t** dsts, const unsigned long long* tc_table,
-                                     unsigned long long* tc_addr, unsigned long long* emask,
-                                     int* status, unsigned long long* syn_addr,
+                                     uint8_t** dsts, const unsigned long long* tc_table, int* status,
                                      const uint8_t* src, const uint8_t* par,
-                                     unsigned long long* dir_addr, uint8_t* jit_coef,
-                                     hipStream_t st)
+                                     unsigned long long* dir_addr, uint8_t* jit_coef, hipStream_t st)
 {
     if (k <= 0 || k > 250 || e <= 0 || e > (jit_coef ? 63 : 32) || k + e > 250 ||
-        (!jit_coef && (!tc_table || (!dir_addr && (!tc_addr || !syn_addr)))))
+        (!jit_coef && (!tc_table || !dir_addr)))
         return hipErrorInvalidValue;
     static bool attr_set = false;
     if (!attr_set) {
@@ -1155,7 +1042,7 @@ hipError_t launch_decode_prepare_syn(int k, int e, long long blocks, const uint8
     }
     hipLaunchKernelGGL(k_decode_prepare_syn, dim3((unsigned)blocks), dim3(256),
                        decode_prepare_syn_lds_bytes(e), st, k, e, err, out, out_pitch, srcs, dsts,
-                       tc_table, tc_addr, emask, status, syn_addr, src, par, dir_addr, jit_coef);
+                       tc_table, status, src, par, dir_addr, jit_coef);
     return hipGetLastError();
 }
 

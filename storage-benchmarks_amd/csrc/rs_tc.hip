@@ -89,34 +89,15 @@ __global__ void k_tc_handlers(unsigned long long* out)
     }
 }
 
-// Phase accounting for tools/tc_profile.hip (compiled in only there, with
-// -DRSGPU_TC_PROF): per-wave s_memtime sums of each phase, added into
-// rsgpu_tc_prof[phase] at the end of the wave.
-#ifdef RSGPU_TC_PROF
-__device__ unsigned long long rsgpu_tc_prof[8];
-#define TC_PROF_DECL unsigned long long tp_sum[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tp_t = __builtin_amdgcn_s_memtime(), tp_start = tp_t;
-#define TC_PROF_MARK(P)                                    \
-    do {                                                   \
-        const unsigned long long tp_n = __builtin_amdgcn_s_memtime(); \
-        tp_sum[P] += tp_n - tp_t;                          \
-        tp_t = tp_n;                                       \
-    } while (0)
-#define TC_PROF_END                                                                \
-    do {                                                                           \
-        tp_sum[7] = __builtin_amdgcn_s_memtime() - tp_start;                       \
-        if (lane == 0 && (blockIdx.x & 63) == 0)  /* sampled: same-address atomics serialise */ \
-            for (int i = 0; i < 8; ++i)                                            \
-                atomicAdd(&rsgpu_tc_prof[i], tp_sum[i]);                           \
-    } while (0)
-#else
-#define TC_PROF_DECL
-#define TC_PROF_MARK(P) \
-    do {                \
-    } while (0)
-#define TC_PROF_END \
-    do {            \
-    } while (0)
-#endif
+// Instrumentation point of k_rs_tc: the product's TcHooks time nothing;
+// tools/tc_profile.hip instantiates the kernel with a policy whose Timer sums
+// s_memtime per phase.
+struct TcHooks {
+    struct Timer {
+        __device__ void mark(int) {}
+        __device__ void end(int) {}
+    };
+};
 
 // Read accumulator slot S (asm-owned v[64+8S : 64+8S+7]) into W, two planes
 // per v_mov_b64.
@@ -144,7 +125,7 @@ __device__ __forceinline__ void read_slot(uint32_t (&W)[8])
 // amdgpu_num_vgpr(64): the compiler allocates v0..v63 only; the accumulators
 // v64..v127 are touched by asm alone, so they stay put across the loops (the
 // kernel descriptor still reserves 128 VGPRs because the asm names v127).
-template <int NW>
+template <int NW, class H = TcHooks>
 __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_num_vgpr(64))) void k_rs_tc(TcArgs a, int tiles_per_wg)
 {
     // two chunk buffers [C][2 halves][64 lanes] of 16 bytes: 2 x 16 KiB
@@ -191,16 +172,16 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_num_vgpr(64))) void 
             glds32(sload_ptr(srcs + c0 + t), (uint32_t)loff, base + (uint32_t)(t * 2 * 64 * 16));
     };
 
-    TC_PROF_DECL
+    typename H::Timer tp;
     issue(0);
     for (int n = 0; n < total; ++n) {
         const int ch = n % nch;
         const int nt = min(C, k - ch * C);
         uint4* buf = lds[n & 1];
-        TC_PROF_MARK(6);
+        tp.mark(6);
         wait_vm(0);  // this step's own sources, issued behind the previous step's barrier
-        TC_PROF_MARK(0);
-        TC_PROF_MARK(1);
+        tp.mark(0);
+        tp.mark(1);
         // own share of this chunk: bytes -> bit-planes, in place
         for (int t = wave; t < nt; t += NW) {
             uint4 u = buf[(t * 2 + 0) * 64 + lane];
@@ -210,14 +191,14 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_num_vgpr(64))) void 
             buf[(t * 2 + 0) * 64 + lane] = make_uint4(W[0], W[1], W[2], W[3]);
             buf[(t * 2 + 1) * 64 + lane] = make_uint4(W[4], W[5], W[6], W[7]);
         }
-        TC_PROF_MARK(2);
+        tp.mark(2);
         barrier_lds();
         // one barrier per step: every wave is past its dispatch of step
         // n - 1, which read buffer (n + 1) & 1, so the next step's sources
         // may land there now and arrive during this step's dispatch
         if (n + 1 < total)
             issue(n + 1);
-        TC_PROF_MARK(3);
+        tp.mark(3);
         if (ch == 0)
             asm volatile(RSGPU_TC_ZERO ::: RSGPU_TC_ACC_CLOBBERS);
         // the chunk's nt sources: one asm statement (gen_tc_handlers.py)
@@ -243,7 +224,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_num_vgpr(64))) void 
             }
 #undef RSGPU_TC_RUN
         }
-        TC_PROF_MARK(4);
+        tp.mark(4);
         if (ch == nch - 1) {
             // tile done: outputs back to bytes and out (all of this tile's
             // sources were read before the previous barrier: in-place safe)
@@ -264,10 +245,10 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_num_vgpr(64))) void 
                 }(std::make_integer_sequence<int, 8>{});
             }
         }
-        TC_PROF_MARK(5);
+        tp.mark(5);
     }
-    TC_PROF_MARK(6);
-    TC_PROF_END;
+    tp.mark(6);
+    tp.end(lane);
 }
 
 }  // namespace tc

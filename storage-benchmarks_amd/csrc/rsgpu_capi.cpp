@@ -14,59 +14,11 @@
 
 #include "../../include/rsgpu.h"
 #include "gf256.h"
+#include "rsgpu_ctx.h"
 #include "jit_prog.h"
 #include "rs_jit.h"
 #include "rs_kernels.h"
 #include "rs_synth.h"
-
-struct rsgpu_ctx {
-    int device = 0;
-    hipStream_t stream = nullptr;
-    // cross-stream ordering events (rsgpu_set_stream), recycled round-robin
-    std::vector<hipEvent_t> sync_evs;
-    size_t sync_next = 0;
-    // threaded-code kernel (rs_tc.hip): device table of the handler
-    // addresses [slot][coefficient]; tc_state 0 = not probed, 1 = ready,
-    // -1 = unavailable (k_dot_generic serves instead)
-    unsigned long long* d_tc_table = nullptr;
-    unsigned long long h_tc_table[2048] = {};
-    int tc_state = 0;
-    int decode_kernel = RSGPU_DECODE_AUTO;
-    // executable device memory for the generated decode code (rs_jit.h):
-    // grow-only; jit_state 0 = not probed, 1 = pool found, -1 = unavailable
-    void* d_jit = nullptr;
-    size_t jit_bytes = 0;
-    int jit_state = 0;
-    hsa_amd_memory_pool_t jit_pool{};
-    // host-built code of the last shared coefficient matrix (jit_prog.h):
-    // executable copy, its key (k, rows, coefficients) and chunk stride, and
-    // the ordinary device buffer it is staged through
-    int encode_kernel = RSGPU_ENCODE_AUTO;
-    void* d_enc_code = nullptr;
-    size_t enc_code_bytes = 0;
-    std::vector<uint8_t> enc_key;
-    int enc_chunk_stride = 0;
-    void* d_code_stage = nullptr;
-    size_t code_stage_bytes = 0;
-    std::string err;
-    // grow-only device scratch for pointer tables / coefficient tables
-    void* d_scratch = nullptr;
-    size_t scratch_bytes = 0;
-    // pinned host staging for small uploads, guarded by an event
-    void* h_stage = nullptr;
-    size_t stage_bytes = 0;
-    hipEvent_t stage_done = nullptr;
-    bool stage_pending = false;
-    // timing instrumentation
-    bool timing = false;
-    struct Rec {
-        const char* name;
-        hipEvent_t a, b;
-        size_t blocks;
-    };
-    std::vector<Rec> recs;
-    std::vector<hipEvent_t> ev_pool;
-};
 
 namespace {
 
@@ -87,21 +39,6 @@ inline uint8_t hmul(uint8_t a, uint8_t b)
     const GfTables& t = host_gf();
     return (a && b) ? t.exp[t.log[a] + t.log[b]] : 0;
 }
-
-int fail(rsgpu_ctx* ctx, int code, const std::string& msg)
-{
-    if (ctx)
-        ctx->err = msg;
-    return code;
-}
-
-#define RS_HIP(ctx, call)                                                                     \
-    do {                                                                                      \
-        hipError_t e_ = (call);                                                               \
-        if (e_ != hipSuccess)                                                                 \
-            return fail((ctx), RSGPU_ERR_HIP,                                                 \
-                        std::string(#call) + ": " + hipGetErrorString(e_));                   \
-    } while (0)
 
 // Grow the scratch buffer.  Every kernel that may still read the old buffer
 // was enqueued on the context stream, or on an earlier stream the current
@@ -315,6 +252,7 @@ int jit_ensure(rsgpu_ctx* ctx, size_t bytes)
         return fail(ctx, RSGPU_ERR_NOMEM, "executable device allocation failed");
     ctx->d_jit = p;
     ctx->jit_bytes = want;
+    ++ctx->jit_gen;
     RS_HIP(ctx, launch_jit_fill(p, want, ctx->stream));
     return RSGPU_OK;
 }
@@ -586,6 +524,15 @@ int rsgpu_destroy(rsgpu_ctx* ctx)
         hsa_amd_memory_pool_free(ctx->d_enc_code);
     if (ctx->d_code_stage)
         (void)hipFree(ctx->d_code_stage);
+    for (hipStream_t st : {ctx->io_in, ctx->io_out})
+        if (st) {
+            (void)hipStreamSynchronize(st);
+            (void)hipStreamDestroy(st);
+        }
+    if (ctx->d_io)
+        (void)hipFree(ctx->d_io);
+    for (auto e : ctx->io_evs)
+        (void)hipEventDestroy(e);
     delete ctx;
     return RSGPU_OK;
 }
@@ -595,14 +542,21 @@ int rsgpu_set_stream(rsgpu_ctx* ctx, void* s)
     if (!ctx)
         return RSGPU_ERR_ARG;
     hipStream_t ns = (hipStream_t)s;
-    if (ns != ctx->stream) {
-        // everything enqueued on the old stream (kernels reading the scratch
-        // tables among them) is ordered before the new stream's work
-        hipEvent_t ev = sync_event(ctx);
-        RS_HIP(ctx, hipEventRecord(ev, ctx->stream));
-        RS_HIP(ctx, hipStreamWaitEvent(ns, ev, 0));
-    }
+    if (ns == ctx->stream)
+        return RSGPU_OK;
+    // everything enqueued on the old stream (kernels reading the scratch
+    // tables among them) is ordered before the new stream's work.  The
+    // context moves to the new stream even when that cannot be arranged (an
+    // old stream already destroyed): it is never left bound to a dead one;
+    // the error is reported after the move.
+    hipEvent_t ev = sync_event(ctx);
+    hipError_t e = hipEventRecord(ev, ctx->stream);
+    if (e == hipSuccess)
+        e = hipStreamWaitEvent(ns, ev, 0);
     ctx->stream = ns;
+    if (e != hipSuccess)
+        return fail(ctx, RSGPU_ERR_HIP, std::string("rsgpu_set_stream: ordering against the old stream: ") +
+                                            hipGetErrorString(e));
     return RSGPU_OK;
 }
 
@@ -940,7 +894,7 @@ int rsgpu_set_encode_kernel(rsgpu_ctx* ctx, int kernel)
 
 int rsgpu_set_decode_kernel(rsgpu_ctx* ctx, int kernel)
 {
-    if (!ctx || kernel < RSGPU_DECODE_AUTO || kernel > RSGPU_DECODE_GENERATED)
+    if (!ctx || kernel < RSGPU_DECODE_AUTO || kernel > RSGPU_DECODE_GENERATED || kernel == 2)
         return fail(ctx, RSGPU_ERR_ARG, "rsgpu_set_decode_kernel: unknown kernel");
     ctx->decode_kernel = kernel;
     return RSGPU_OK;
@@ -955,7 +909,6 @@ namespace {
 enum class Plan {
     generated,   // k_decode_prepare_syn (closed form, writes code) + k_rs_jit
     one_matrix,  // k_decode_prepare_syn (closed form) + k_rs_tc
-    fused,       // k_decode_prepare_syn (e x e) + k_rs_decode_fused
     general_tc,   // k_decode_prepare (k x k inversion) + k_rs_tc passes
     general_jit,  // k_decode_prepare + per-block generated code, passes of 32 rows
     general_dot   // k_decode_prepare + k_dot_generic (unaligned / odd lengths)
@@ -994,16 +947,14 @@ Plan decode_plan(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch, size_t 
         return Plan::general_dot;
     const int want = ctx->decode_kernel;
     // the closed-form rows need Lambda's e + 1 coefficients in one wave
-    // (e <= 63); the threaded-code and fused kernels take e <= 32
+    // (e <= 63); the threaded-code kernel takes e <= 32
     const bool gen_ok = e <= 63 && jit_probe(ctx) == 1 && want != RSGPU_DECODE_ONE_MATRIX &&
-                        want != RSGPU_DECODE_FUSED && want != RSGPU_DECODE_GENERAL &&
+                        want != RSGPU_DECODE_GENERAL &&
                         (want == RSGPU_DECODE_GENERATED || (len + 2047) / 2048 >= kJitMinTiles);
     if (e > 32 && gen_ok)
         return Plan::generated;
     if (want == RSGPU_DECODE_GENERAL || e > 32)
         return general_plan(ctx, len);
-    if (want == RSGPU_DECODE_FUSED && rs_decode_fused_available(k, e))
-        return Plan::fused;
     if (want == RSGPU_DECODE_ONE_MATRIX || jit_probe(ctx) != 1)
         return Plan::one_matrix;
     // AUTO: generated code only when a block has enough column tiles to
@@ -1017,30 +968,26 @@ Plan decode_plan(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch, size_t 
     return Plan::generated;
 }
 
-// Workspace: [emask B x 16 B | survivor ptrs B x k | output ptrs B x e |
-// coefficient region], the region sized for the largest consumer: k_rs_tc
-// handler addresses (pass layout; the fused kernel's e x e + (k-e) x e
-// tables are no larger) or the v_perm tables.
+// Workspace: [survivor ptrs B x k | output ptrs B x e | coefficient region],
+// the region sized for the largest consumer: k_rs_tc handler addresses (pass
+// layout), the v_perm tables, or the generated decode's e x k rows.
 struct WsLayout {
-    size_t surv, outp, tab, tab2, total;
+    size_t surv, outp, tab, total;
 };
 
 WsLayout ws_layout(int k, int e, size_t blocks)
 {
     WsLayout w{};
-    size_t o = align_up(16 * blocks, 256);
+    size_t o = 0;
     w.surv = o;
     o = align_up(o + sizeof(void*) * (size_t)k * blocks, 256);
     w.outp = o;
     o = align_up(o + sizeof(void*) * (size_t)e * blocks, 256);
     w.tab = o;
-    // fused: syndrome-phase addresses after the e x e ones
-    w.tab2 = align_up(o + sizeof(unsigned long long) * (size_t)e * tc_rows_per_pass(e) * blocks, 256);
     const size_t tc_bytes = sizeof(unsigned long long) * (size_t)tc_table_elems(k, e) * blocks;
-    const size_t fused_bytes = (w.tab2 - o) + sizeof(unsigned long long) * (size_t)(k > e ? k - e : 0) *
-                                                  tc_rows_per_pass(e) * blocks;
     const size_t dot_bytes = (sizeof(uint4) + sizeof(uint32_t)) * (size_t)k * rows_pad_for(e) * blocks;
-    w.total = align_up(o + std::max({tc_bytes, fused_bytes, dot_bytes}), 256);
+    const size_t jit_bytes = (size_t)e * k * blocks;
+    w.total = align_up(o + std::max({tc_bytes, dot_bytes, jit_bytes}), 256);
     return w;
 }
 
@@ -1057,9 +1004,16 @@ size_t decode_code_bytes(int k, int e, size_t blocks)
 }
 
 // k_jit_emit / k_jitw_emit: the code of every block from its decode rows
-// coef [B][e][k] into the context's executable memory
-int emit_decode_code(rsgpu_ctx* ctx, int k, int e, size_t blocks, const uint8_t* coef, const int* d_status)
+// coef [B][e][k] into the context's executable memory, which from now on
+// belongs to this (k, e, blocks, workspace) prepare
+int emit_decode_code(rsgpu_ctx* ctx, int k, int e, size_t blocks, const uint8_t* coef, const int* d_status,
+                     const void* ws)
 {
+    ctx->jit_key.k = k;
+    ctx->jit_key.e = e;
+    ctx->jit_key.blocks = blocks;
+    ctx->jit_key.ws = ws;
+    ctx->jit_key.gen = ++ctx->jit_gen;
     if (jitw_rows(e)) {
         KTimer ke(ctx, jitw_rows(e) == 16 ? "k_jit16_emit" : jitw_rows(e) == 12 ? "k_jit12_emit" : "k_jit10_emit",
                   blocks);
@@ -1075,11 +1029,18 @@ int emit_decode_code(rsgpu_ctx* ctx, int k, int e, size_t blocks, const uint8_t*
 // k_rs_jitw in one launch (decode_code_bytes), or k_rs_jit in passes of
 // <= 32 rows: block b, pass p, wave w, chunk ch at d_jit + b block_stride +
 // ((4 p + w) nch + ch) chunk_stride (k_jit_emit's layout).
-int jit_decode_launch(rsgpu_ctx* ctx, int k, int e, size_t len, size_t blocks,
+int jit_decode_launch(rsgpu_ctx* ctx, int k, int e, size_t len, size_t blocks, const void* ws,
                       const uint8_t* const* d_srcs, uint8_t* const* d_dsts, const int* d_status)
 {
     if (!ctx->d_jit || ctx->jit_bytes < decode_code_bytes(k, e, blocks))
         return fail(ctx, RSGPU_ERR_ARG, "rsgpu_decode_apply: no prepared decode code");
+    // the code must be the one this workspace's prepare emitted, untouched
+    // since: another prepare, a decode_general or a regrow rewrites it
+    if (ctx->jit_key.gen != ctx->jit_gen || ctx->jit_key.k != k || ctx->jit_key.e != e ||
+        ctx->jit_key.blocks != blocks || ctx->jit_key.ws != ws)
+        return fail(ctx, RSGPU_ERR_ARG,
+                    "rsgpu_decode_apply: the generated code belongs to another prepare "
+                    "(re-run rsgpu_decode_prepare for this workspace)");
     if (jitw_rows(e)) {
         JitArgs j{};
         j.srcs = d_srcs;
@@ -1172,7 +1133,7 @@ int general_prepare(rsgpu_ctx* ctx, Plan plan, int k, int m, int nerrs, bool ori
         RS_HIP(ctx, launch_decode_prepare(p, ctx->stream));
     }
     if (plan == Plan::general_jit)
-        return emit_decode_code(ctx, k, nerrs, blocks, p.coef_out, d_status);
+        return emit_decode_code(ctx, k, nerrs, blocks, p.coef_out, d_status, d_workspace);
     return RSGPU_OK;
 }
 
@@ -1182,7 +1143,7 @@ int general_apply(rsgpu_ctx* ctx, Plan plan, int k, int nerrs, size_t len, size_
     const WsLayout w = ws_layout(k, nerrs, blocks);
     char* ws = (char*)d_workspace;
     if (plan == Plan::general_jit)
-        return jit_decode_launch(ctx, k, nerrs, len, blocks, (const uint8_t* const*)(ws + w.surv),
+        return jit_decode_launch(ctx, k, nerrs, len, blocks, ws, (const uint8_t* const*)(ws + w.surv),
                                  (uint8_t* const*)(ws + w.outp), d_status);
     if (plan == Plan::general_tc)
         return tc_launch(ctx, "k_rs_tc(decode)", (const uint8_t* const*)(ws + w.surv),
@@ -1236,10 +1197,10 @@ int rsgpu_decode_prepare(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch,
         return fail(ctx, RSGPU_ERR_ARG, "rsgpu_decode_prepare: at most 65535 blocks per call "
                                         "(rsgpu_decode_blocks slices larger batches)");
     const Plan plan = decode_plan(ctx, k, e, len, pitch, blocks, d_src, d_parity, d_out);
-    if (plan == Plan::one_matrix || plan == Plan::fused || plan == Plan::generated) {
+    if (plan == Plan::one_matrix || plan == Plan::generated) {
         const WsLayout w = ws_layout(k, e, blocks);
         char* ws = (char*)d_workspace;
-        const bool one = plan == Plan::one_matrix, gen = plan == Plan::generated;
+        const bool gen = plan == Plan::generated;
         if (gen) {
             rc = jit_ensure(ctx, decode_code_bytes(k, e, blocks));
             if (rc)
@@ -1250,14 +1211,11 @@ int rsgpu_decode_prepare(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch,
             RS_HIP(ctx, launch_decode_prepare_syn(
                             k, e, (long long)blocks, d_err, d_out, (long long)pitch,
                             (const uint8_t**)(ws + w.surv), (uint8_t**)(ws + w.outp), ctx->d_tc_table,
-                            plan == Plan::fused ? (unsigned long long*)(ws + w.tab) : nullptr,
-                            (unsigned long long*)ws, d_status,
-                            plan == Plan::fused ? (unsigned long long*)(ws + w.tab2) : nullptr, d_src,
-                            d_parity, one ? (unsigned long long*)(ws + w.tab) : nullptr,
+                            d_status, d_src, d_parity, gen ? nullptr : (unsigned long long*)(ws + w.tab),
                             gen ? (uint8_t*)(ws + w.tab) : nullptr, ctx->stream));
         }
         if (gen)  // the decode rows [B][e][k] sit in the coefficient region
-            return emit_decode_code(ctx, k, e, blocks, (const uint8_t*)(ws + w.tab), d_status);
+            return emit_decode_code(ctx, k, e, blocks, (const uint8_t*)(ws + w.tab), d_status, ws);
         return RSGPU_OK;
     }
     return general_prepare(ctx, plan, k, k + e, e, true, pitch, blocks, nullptr, d_src, d_parity,
@@ -1283,7 +1241,7 @@ int rsgpu_decode_apply(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch, s
     char* ws = (char*)d_workspace;
     if (plan == Plan::generated)
         // one matrix, the block's generated code (rs_jit.hip), passes of 32 rows
-        return jit_decode_launch(ctx, k, e, len, blocks, (const uint8_t* const*)(ws + w.surv),
+        return jit_decode_launch(ctx, k, e, len, blocks, ws, (const uint8_t* const*)(ws + w.surv),
                                  (uint8_t* const*)(ws + w.outp), d_status);
     if (plan == Plan::one_matrix)
         // one pass, one matrix over the k - e survivors and the e parity rows
@@ -1291,16 +1249,6 @@ int rsgpu_decode_apply(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch, s
                          (uint8_t* const*)(ws + w.outp), (const unsigned long long*)(ws + w.tab),
                          (long long)k * tc_rows_per_pass(e), k, e, (long long)len,
                          (long long)blocks, d_status);
-    if (plan == Plan::fused) {
-        // one pass: syndromes + solve per column tile (rs_decode_fused.hip)
-        KTimer kt(ctx, "k_rs_decode_fused", blocks);
-        RS_HIP(ctx, launch_rs_decode_fused(k, e, d_src, d_parity, d_out, (long long)pitch,
-                                           (long long)len, (long long)blocks, (const uint64_t*)ws,
-                                           (const unsigned long long*)(ws + w.tab),
-                                           (const unsigned long long*)(ws + w.tab2), d_status,
-                                           ctx->stream));
-        return RSGPU_OK;
-    }
     const bool aligned = ((uintptr_t)d_src % 16 == 0) && ((uintptr_t)d_parity % 16 == 0) &&
                          ((uintptr_t)d_out % 16 == 0) && (pitch % 16 == 0);
     return general_apply(ctx, plan, k, e, len, pitch, blocks, aligned, d_workspace, d_status);

@@ -1,0 +1,97 @@
+// rsgpu_ctx.h -- the context behind include/rsgpu.h's opaque rsgpu_ctx
+// (internal to librsgpu): its stream, grow-only device scratch, generated-code
+// memory, the host-resident pipeline's streams and staging, and timing.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <hsa/hsa.h>
+#include <hsa/hsa_ext_amd.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/rsgpu.h"
+
+struct rsgpu_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    // cross-stream ordering events (rsgpu_set_stream), recycled round-robin
+    std::vector<hipEvent_t> sync_evs;
+    size_t sync_next = 0;
+    // threaded-code kernel (rs_tc.hip): device table of the handler
+    // addresses [slot][coefficient]; tc_state 0 = not probed, 1 = ready,
+    // -1 = unavailable (k_dot_generic serves instead)
+    unsigned long long* d_tc_table = nullptr;
+    unsigned long long h_tc_table[2048] = {};
+    int tc_state = 0;
+    int decode_kernel = RSGPU_DECODE_AUTO;
+    // executable device memory for the generated decode code (rs_jit.h):
+    // grow-only; jit_state 0 = not probed, 1 = pool found, -1 = unavailable
+    void* d_jit = nullptr;
+    size_t jit_bytes = 0;
+    int jit_state = 0;
+    // the code in d_jit belongs to ONE prepare: its key, and a generation
+    // bumped by every emission and reallocation, checked by the apply
+    unsigned long long jit_gen = 0;
+    struct {
+        int k = 0, e = 0;
+        size_t blocks = 0;
+        const void* ws = nullptr;
+        unsigned long long gen = 0;
+    } jit_key;
+    hsa_amd_memory_pool_t jit_pool{};
+    // host-built code of the last shared coefficient matrix (jit_prog.h):
+    // executable copy, its key (k, rows, coefficients) and chunk stride, and
+    // the ordinary device buffer it is staged through
+    int encode_kernel = RSGPU_ENCODE_AUTO;
+    void* d_enc_code = nullptr;
+    size_t enc_code_bytes = 0;
+    std::vector<uint8_t> enc_key;
+    int enc_chunk_stride = 0;
+    void* d_code_stage = nullptr;
+    size_t code_stage_bytes = 0;
+    std::string err;
+    // grow-only device scratch for pointer tables / coefficient tables
+    void* d_scratch = nullptr;
+    size_t scratch_bytes = 0;
+    // pinned host staging for small uploads, guarded by an event
+    void* h_stage = nullptr;
+    size_t stage_bytes = 0;
+    hipEvent_t stage_done = nullptr;
+    bool stage_pending = false;
+    // timing instrumentation
+    bool timing = false;
+    struct Rec {
+        const char* name;
+        hipEvent_t a, b;
+        size_t blocks;
+    };
+    std::vector<Rec> recs;
+    std::vector<hipEvent_t> ev_pool;
+    // host-resident calls (rsgpu_encode_blocks_host / _decode_blocks_host):
+    // copy-in and copy-out streams beside `stream`, grow-only device staging
+    // slots, and the events that chain the three stages
+    hipStream_t io_in = nullptr, io_out = nullptr;
+    void* d_io = nullptr;
+    size_t io_bytes = 0;
+    std::vector<hipEvent_t> io_evs;
+};
+
+
+namespace rsgpu {
+
+inline int fail(rsgpu_ctx* ctx, int code, const std::string& msg)
+{
+    if (ctx)
+        ctx->err = msg;
+    return code;
+}
+
+}  // namespace rsgpu
+
+#define RS_HIP(ctx, call)                                                                     \
+    do {                                                                                      \
+        hipError_t e_ = (call);                                                               \
+        if (e_ != hipSuccess)                                                                 \
+            return ::rsgpu::fail((ctx), RSGPU_ERR_HIP,                                        \
+                                 std::string(#call) + ": " + hipGetErrorString(e_));          \
+    } while (0)

@@ -6,7 +6,7 @@
 // line as  symbols:symbol_size:erased ...
 //
 //   --decode-kernel K   rsgpu_set_decode_kernel: auto | generated |
-//                       one_matrix | fused | general
+//                       one_matrix | general
 //   --poison            after encode_all, overwrite every erased original row
 //                       on the device with 0xA5 (keeping a host copy): the
 //                       reference's decoder never reads them (isa.cpp:193-
@@ -102,7 +102,6 @@ int main(int argc, char** argv)
         } else if (a == "--decode-kernel" && i + 1 < argc) {
             const std::string k = argv[++i];
             kernel = k == "one_matrix" ? RSGPU_DECODE_ONE_MATRIX
-                   : k == "fused"      ? RSGPU_DECODE_FUSED
                    : k == "general"    ? RSGPU_DECODE_GENERAL
                    : k == "generated"  ? RSGPU_DECODE_GENERATED
                                        : RSGPU_DECODE_AUTO;

@@ -1,16 +1,33 @@
 // rs_throughput.cpp -- command-line peer of benchmark/isa_throughput
 // (isa.cpp:261-330) running the MI355X engine.  Same options
 // (--symbols, --loss_rate, --symbol_size, --type as multitoken lists, --runs),
-// plus --blocks, --seed, --device.  Results print as a table and optionally
-// as gauge-compatible CSV / JSON (columns: testcase, benchmark, symbols,
-// symbol_size, loss_rate, type, erased_symbols, goodput -- the names
-// plot_storage_benchmarks.py reads) with extra blocks/seconds columns.
+// plus --blocks, --seed, --device, and:
+//   --resident device|host  where the blocks live between calls (host: the
+//                           reference's layout, copies inside the timed
+//                           regions; gpu_plugin.hpp `resident`)
+//   --gpus N                one host thread per GPU (devices device ..
+//                           device+N-1), each with its own context and its own
+//                           `blocks` blocks (weak scaling, no exchange); the
+//                           threads start every timed region on a barrier
+//                           and a run's goodput is all GPUs' bytes over the
+//                           slowest GPU's time
+//   --same-device           every thread on `device` (tests the fan-out and
+//                           the concurrent contexts on a one-GPU box)
+// Results print as a table and optionally as gauge-compatible CSV / JSON
+// (columns: testcase, benchmark, symbols, symbol_size, loss_rate, type,
+// erased_symbols, goodput -- the names plot_storage_benchmarks.py reads) with
+// extra blocks/gpus/seconds columns.
+#include <algorithm>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <exception>
 #include <fstream>
 #include <memory>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "gpu_plugin.hpp"
@@ -23,15 +40,51 @@ static void usage()
     std::printf(
         "rs_throughput [--symbols N...] [--loss_rate R...] [--symbol_size P...]\n"
         "              [--type encoder|decoder...] [--runs N] [--blocks B]\n"
-        "              [--seed S] [--device D] [--csv_file F] [--json_file F]\n");
+        "              [--seed S] [--device D] [--resident device|host]\n"
+        "              [--gpus N] [--same-device] [--csv_file F] [--json_file F]\n");
 }
+
+// A reusable barrier for the per-GPU threads; a thread that fails breaks it
+// so that the others stop waiting.
+struct barrier {
+    explicit barrier(int n) : n(n) {}
+    void wait()
+    {
+        std::unique_lock<std::mutex> lk(m);
+        if (broken)
+            throw std::runtime_error("another GPU thread failed");
+        const unsigned long long g = gen;
+        if (++count == n) {
+            count = 0;
+            ++gen;
+            cv.notify_all();
+            return;
+        }
+        cv.wait(lk, [&] { return gen != g || broken; });
+        if (broken)
+            throw std::runtime_error("another GPU thread failed");
+    }
+    void brk()
+    {
+        std::lock_guard<std::mutex> lk(m);
+        broken = true;
+        cv.notify_all();
+    }
+    std::mutex m;
+    std::condition_variable cv;
+    int n, count = 0;
+    unsigned long long gen = 0;
+    bool broken = false;
+};
 
 int main(int argc, char** argv)
 {
     options o;
     uint32_t blocks = 1;
     uint64_t seed = 1;
-    int device = 0;
+    int device = 0, gpus = 1;
+    bool same_device = false;
+    resident where = resident::device;
     std::string csv, json;
     auto take = [&](int& i, auto fn) {
         while (i + 1 < argc && std::strncmp(argv[i + 1], "--", 2) != 0)
@@ -59,6 +112,15 @@ int main(int argc, char** argv)
             seed = std::strtoull(argv[++i], nullptr, 10);
         } else if (a == "--device" && i + 1 < argc) {
             device = std::atoi(argv[++i]);
+        } else if (a == "--gpus" && i + 1 < argc) {
+            gpus = std::atoi(argv[++i]);
+        } else if (a == "--same-device") {
+            same_device = true;
+        } else if (a == "--resident" && i + 1 < argc) {
+            const std::string v = argv[++i];
+            if (v != "host" && v != "device")
+                return usage(), 2;
+            where = v == "host" ? resident::host : resident::device;
         } else if (a == "--csv_file" && i + 1 < argc) {
             csv = argv[++i];
         } else if (a == "--json_file" && i + 1 < argc) {
@@ -68,42 +130,94 @@ int main(int argc, char** argv)
             return a == "--help" ? 0 : 2;
         }
     }
-    auto session = std::make_shared<gpu_session>(device);
-    std::vector<result_row> rows;
-    uint64_t run_id = 0;
-    for (const auto& cs : expand(o)) {
-        throughput_benchmark<gpu_encoder, gpu_decoder> tb(
-            [&](const config_set& c) {
-                return std::make_shared<gpu_encoder>(session, c.symbols, c.symbol_size,
-                                                     c.erased_symbols, blocks, seed, run_id * blocks);
-            },
-            [&](const config_set& c) {
-                return std::make_shared<gpu_decoder>(session, c.symbols, c.symbol_size,
-                                                     c.erased_symbols, blocks, seed, run_id * blocks);
-            });
-        for (uint32_t r = 0; r < o.runs; ++r, ++run_id) {
-            tb.setup(cs);
-            result_row row = tb.run(r);
-            if (!row.accepted) {
-                std::printf("measurement rejected (incomplete decode)\n");
-                continue;
+    if (gpus < 1 || blocks < 1)
+        return usage(), 2;
+    // every (configuration, run) in order; each GPU thread runs all of them
+    std::vector<std::pair<config_set, uint32_t>> plan;
+    for (const auto& cs : expand(o))
+        for (uint32_t r = 0; r < o.runs; ++r)
+            plan.push_back({cs, r});
+    std::vector<std::vector<result_row>> per(gpus, std::vector<result_row>(plan.size()));
+    barrier bar(gpus);
+    std::vector<std::string> errors(gpus);
+    auto worker = [&](int t) {
+        try {
+            auto session = std::make_shared<gpu_session>(same_device ? device : device + t);
+            for (size_t i = 0; i < plan.size(); ++i) {
+                const config_set& cs = plan[i].first;
+                // distinct blocks per (run, GPU): erasures and data follow the
+                // global block index
+                const uint64_t block0 = ((uint64_t)i * gpus + t) * blocks;
+                throughput_benchmark<gpu_encoder, gpu_decoder> tb(
+                    [&](const config_set& c) {
+                        return std::make_shared<gpu_encoder>(session, c.symbols, c.symbol_size,
+                                                             c.erased_symbols, blocks, seed, block0, where);
+                    },
+                    [&](const config_set& c) {
+                        return std::make_shared<gpu_decoder>(session, c.symbols, c.symbol_size,
+                                                             c.erased_symbols, blocks, seed, block0, where);
+                    });
+                if (gpus > 1)
+                    tb.before_timed = [&] { bar.wait(); };
+                tb.setup(cs);
+                per[t][i] = tb.run(plan[i].second);
             }
-            std::printf("symbols=%u symbol_size=%u loss_rate=%g type=%s erased=%u blocks=%u "
-                        "run=%u goodput=%.1f MB/s (%.3f GiB/s, %.3f ms)\n",
-                        cs.symbols, cs.symbol_size, cs.loss_rate, cs.type.c_str(),
-                        cs.erased_symbols, blocks, r, row.goodput,
-                        row.bytes / row.seconds / 1073741824.0, row.seconds * 1e3);
-            rows.push_back(row);
+        } catch (const std::exception& ex) {
+            errors[t] = ex.what();
+            bar.brk();
         }
+    };
+    if (gpus == 1) {
+        worker(0);
+    } else {
+        std::vector<std::thread> th;
+        for (int t = 0; t < gpus; ++t)
+            th.emplace_back(worker, t);
+        for (auto& x : th)
+            x.join();
+    }
+    int rc = 0;
+    for (int t = 0; t < gpus; ++t)
+        if (!errors[t].empty()) {
+            std::fprintf(stderr, "gpu thread %d: %s\n", t, errors[t].c_str());
+            rc = 1;
+        }
+    if (rc)
+        return rc;
+    std::vector<result_row> rows;
+    for (size_t i = 0; i < plan.size(); ++i) {
+        // the job's row: every GPU's bytes over the slowest GPU's time
+        result_row row = per[0][i];
+        row.bytes = 0;
+        row.seconds = 0;
+        for (int t = 0; t < gpus; ++t) {
+            row.bytes += per[t][i].bytes;
+            row.seconds = std::max(row.seconds, per[t][i].seconds);
+            row.accepted = row.accepted && per[t][i].accepted;
+        }
+        row.goodput = (double)row.bytes / (row.seconds * 1e6);
+        const config_set& cs = row.cs;
+        if (!row.accepted) {
+            std::printf("measurement rejected (incomplete decode)\n");
+            rc = 3;
+            continue;
+        }
+        std::printf("symbols=%u symbol_size=%u loss_rate=%g type=%s erased=%u blocks=%u gpus=%d "
+                    "resident=%s run=%u goodput=%.1f MB/s (%.3f GiB/s, %.3f ms)\n",
+                    cs.symbols, cs.symbol_size, cs.loss_rate, cs.type.c_str(), cs.erased_symbols, blocks, gpus,
+                    where == resident::host ? "host" : "device", row.run, row.goodput,
+                    row.bytes / row.seconds / 1073741824.0, row.seconds * 1e3);
+        rows.push_back(row);
     }
     if (!csv.empty()) {
         std::ofstream f(csv);
-        f << "testcase,benchmark,symbols,symbol_size,loss_rate,type,erased_symbols,blocks,run,"
-             "seconds,goodput\n";
+        f << "testcase,benchmark,symbols,symbol_size,loss_rate,type,erased_symbols,blocks,gpus,"
+             "resident,run,seconds,goodput\n";
         for (const auto& r : rows)
             f << "MI355X,ErasureCode," << r.cs.symbols << "," << r.cs.symbol_size << ","
               << r.cs.loss_rate << "," << r.cs.type << "," << r.cs.erased_symbols << "," << blocks
-              << "," << r.run << "," << r.seconds << "," << r.goodput << "\n";
+              << "," << gpus << "," << (where == resident::host ? "host" : "device") << "," << r.run
+              << "," << r.seconds << "," << r.goodput << "\n";
     }
     if (!json.empty()) {
         std::ofstream f(json);
@@ -114,11 +228,12 @@ int main(int argc, char** argv)
               << r.cs.symbols << ", \"symbol_size\": " << r.cs.symbol_size
               << ", \"loss_rate\": " << r.cs.loss_rate << ", \"type\": \"" << r.cs.type
               << "\", \"erased_symbols\": " << r.cs.erased_symbols << ", \"blocks\": " << blocks
-              << ", \"run\": " << r.run << ", \"seconds\": " << r.seconds
+              << ", \"gpus\": " << gpus << ", \"resident\": \""
+              << (where == resident::host ? "host" : "device") << "\", \"run\": " << r.run << ", \"seconds\": " << r.seconds
               << ", \"goodput\": " << r.goodput << "}" << (i + 1 < rows.size() ? "," : "")
               << "\n";
         }
         f << "]\n";
     }
-    return 0;
+    return rc;
 }

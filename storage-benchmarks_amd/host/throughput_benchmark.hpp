@@ -105,8 +105,14 @@ struct throughput_benchmark {
             m_recovered_symbols += (uint64_t)m_cs.erased_symbols * m_encoder->blocks();
     }
 
+    // Called right before each timed region: the multi-GPU runner's barrier,
+    // so every GPU's thread starts its region together.
+    std::function<void()> before_timed;
+
     double run_timed(const std::function<void()>& f)
     {
+        if (before_timed)
+            before_timed();
         auto t0 = std::chrono::steady_clock::now();
         f();
         auto t1 = std::chrono::steady_clock::now();

@@ -46,7 +46,7 @@ ERRORS = {-1: "RSGPU_ERR_ARG", -2: "RSGPU_ERR_HIP", -3: "RSGPU_ERR_SINGULAR",
           -4: "RSGPU_ERR_NOMEM", -5: "RSGPU_ERR_UNSUPPORTED"}
 MAX_SOURCES = 250  # TEST_SOURCES, isa.cpp:25-27
 # rsgpu_set_decode_kernel choices (include/rsgpu.h)
-DECODE_KERNELS = {"auto": 0, "one_matrix": 1, "fused": 2, "general": 3, "generated": 4}
+DECODE_KERNELS = {"auto": 0, "one_matrix": 1, "general": 3, "generated": 4}
 # rsgpu_set_encode_kernel choices (include/rsgpu.h)
 ENCODE_KERNELS = {"auto": 0, "compiled": 1, "generated": 2, "threaded": 3}
 
@@ -92,6 +92,10 @@ _SIGS = {
                                        vp]),
     "rsgpu_decode_apply": (C.c_int, [vp, C.c_int, C.c_int, sz, sz, sz, vp, vp, vp, vp, vp]),
     "rsgpu_verify_blocks": (C.c_int, [vp, C.c_int, C.c_int, sz, sz, sz, vp, vp, vp, vp]),
+    "rsgpu_host_alloc": (C.c_int, [vp, C.POINTER(vp), sz]),
+    "rsgpu_host_free": (C.c_int, [vp, vp]),
+    "rsgpu_encode_blocks_host": (C.c_int, [vp, C.c_int, C.c_int, sz, sz, sz, vp, vp, vp]),
+    "rsgpu_decode_blocks_host": (C.c_int, [vp, C.c_int, C.c_int, sz, sz, sz, vp, vp, vp, vp, vp]),
     "rsgpu_fill_synthetic": (C.c_int, [vp, vp, sz, sz, sz, C.c_uint64, C.c_uint64]),
     "rsgpu_erasure_patterns": (C.c_int, [C.c_uint64, C.c_uint64, sz, C.c_int, C.c_int, vp]),
 }
@@ -238,8 +242,8 @@ class Context:
                    "rsgpu_set_encode_kernel")
 
     def set_decode_kernel(self, kernel: str) -> None:
-        """Decode kernel of decode_blocks: auto | one_matrix | fused | general
-        (include/rsgpu.h rsgpu_set_decode_kernel)."""
+        """Decode kernel of decode_blocks: auto | one_matrix | general |
+        generated (include/rsgpu.h rsgpu_set_decode_kernel)."""
         self.check(lib().rsgpu_set_decode_kernel(self._h, DECODE_KERNELS[kernel]),
                    "rsgpu_set_decode_kernel")
 
@@ -302,6 +306,23 @@ class Context:
         self.check(lib().rsgpu_decode_apply(self._h, k, e, length, pitch, blocks, _ptr(d_src),
                                             _ptr(d_par), _ptr(d_out), _ptr(d_ws), _ptr(d_status)),
                    "rsgpu_decode_apply")
+
+    # host-resident calls (include/rsgpu.h): numpy arrays or pinned torch
+    # CPU tensors; synchronous
+    def encode_blocks_host(self, k, e, length, pitch, blocks, h_src, h_par, coef=None) -> None:
+        cptr = None
+        if coef is not None:
+            coef = np.ascontiguousarray(coef, np.uint8)
+            cptr = coef.ctypes.data
+        self.check(lib().rsgpu_encode_blocks_host(self._h, k, e, length, pitch, blocks, _ptr(h_src),
+                                                  _ptr(h_par), cptr), "rsgpu_encode_blocks_host")
+
+    def decode_blocks_host(self, k, e, length, pitch, blocks, h_src, h_par, h_err, h_out,
+                           h_status=None) -> None:
+        self.check(lib().rsgpu_decode_blocks_host(self._h, k, e, length, pitch, blocks, _ptr(h_src),
+                                                  _ptr(h_par), _ptr(h_err), _ptr(h_out),
+                                                  None if h_status is None else _ptr(h_status)),
+                   "rsgpu_decode_blocks_host")
 
     def decode_general(self, k, m, length, pitch, blocks, encode_matrix, d_src, d_par, d_err, nerrs,
                        d_out, d_ws, d_status) -> None:

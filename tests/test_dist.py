@@ -75,3 +75,15 @@ def test_two_rank_shards_and_max_time(tmp_path):
 def test_single_rank_reduce_is_identity():
     assert bench.reduce_max_time(0.25, 1, torch.device("cpu")) == 0.25
     assert bench.shard(3, 1024) == (3072, 1024)
+
+
+@pytest.mark.parametrize("total,world", [(2500, 2), (2500, 3), (7, 8), (1 << 20, 8), (5, 1)])
+def test_split_covers_every_block_once(total, world):
+    """C4's 2^20 blocks (or any --blocks) over the ranks: contiguous, disjoint
+    shares that cover every block; sizes differ by at most one (no remainder
+    is dropped)."""
+    shares = [bench.split(total, r, world) for r in range(world)]
+    owned = [b for b0, n in shares for b in range(b0, b0 + n)]
+    assert owned == list(range(total))
+    sizes = [n for _, n in shares]
+    assert max(sizes) - min(sizes) <= 1

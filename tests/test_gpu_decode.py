@@ -28,7 +28,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 GOLD = json.load(open(os.path.join(HERE, "golden", "golden.json")))
 BIN = os.path.join(ROOT, "storage-benchmarks_amd", "bin")
-KERNELS = ["auto", "generated", "one_matrix", "fused", "general"]
+KERNELS = ["auto", "generated", "one_matrix", "general"]
 
 
 def sha(b):
@@ -98,8 +98,8 @@ GEOMS = [(16, 4, 1000000, 2), (64, 32, 1000000, 2), (100, 20, 1000000, 2), (16, 
 @pytest.mark.parametrize("kernel", KERNELS)
 @pytest.mark.parametrize("k,e,L,B", GEOMS, ids=lambda v: str(v))
 def test_poisoned_decode_every_kernel(ctx, kernel, k, e, L, B):
-    """Every decode kernel (one-matrix closed form, fused syndrome + solve,
-    the general k x k inversion, and the automatic choice) recovers the
+    """Every decode kernel (one-matrix closed form, generated code, the
+    general k x k inversion, and the automatic choice) recovers the
     originals with the erased rows poisoned, at the BASELINE geometries
     (C2, C3, C5, C1 golden, C4) and general codes (k up to 200, e up to 64
     via row passes, e == k)."""
@@ -130,11 +130,12 @@ def test_poisoned_decode_unaligned_lengths(ctx, kernel):
 
 
 def test_poisoned_host_io_pipelined(ctx):
-    """bench.host_io_pipelined ships only the survivors and poisons the
-    device copies of the erased rows before its decode leg."""
+    """bench.host_io_pipelined poisons the erased rows in host memory before
+    its decode leg: the library ships only the survivors (full-length rows:
+    runs of consecutive survivors)."""
     sys.path.insert(0, ROOT)
     import bench
-    r = bench.host_io_pipelined(rsgpu, ctx, 16, 8, 64000, 6, seed=3, chunk=4, reps=1)
+    r = bench.host_io_pipelined(rsgpu, ctx, 16, 8, 200000, 6, seed=3, reps=1)
     assert r["verified"] and r["blocks"] == 6 and r["poisoned"]
 
 
@@ -451,3 +452,149 @@ def test_auto_decode_kernel_by_batch_work(ctx, blocks, name):
     ctx.timing_enable(False)
     assert ok
     assert name in names and names[-1] == name, names
+
+
+def test_generated_apply_checks_its_prepare(ctx):
+    """The generated decode keeps ONE prepare's code per context: prepare(A),
+    prepare(B), apply(A) must fail (RSGPU_ERR_ARG, nothing launched) instead
+    of running B's code over A's rows; apply(B) then works, and A works again
+    after its own prepare.  Both recoveries are checked with the erased rows
+    poisoned."""
+    k, e, L = 64, 32, 1 << 17
+    ctx.set_decode_kernel("generated")
+    try:
+        encs = [rsgpu.GpuEncoder(k, L, e, blocks=B, seed=s, ctx=ctx) for B, s in ((3, 41), (2, 43))]
+        decs = [rsgpu.GpuDecoder(k, L, e, blocks=B, seed=s, ctx=ctx) for B, s in ((3, 41), (2, 43))]
+        for enc in encs:
+            enc.encode_all()
+        torch.cuda.synchronize()
+
+        def prep(i):
+            enc, dec = encs[i], decs[i]
+            ctx.decode_prepare(k, e, L, enc.pitch, enc.B, enc.src, enc.par, dec.err, dec.out,
+                               dec.ws, dec.status)
+
+        def apply(i):
+            enc, dec = encs[i], decs[i]
+            ctx.decode_apply(k, e, L, enc.pitch, enc.B, enc.src, enc.par, dec.out, dec.ws,
+                             dec.status)
+
+        saved = [poison_rows(enc.src.view(enc.B, k, enc.pitch), dec.err_host, L)
+                 for enc, dec in zip(encs, decs)]
+        prep(0)
+        prep(1)
+        with pytest.raises(rsgpu.RsGpuError, match="another prepare"):
+            apply(0)
+        apply(1)
+        prep(0)
+        apply(0)
+        torch.cuda.synchronize()
+        for enc, dec, sv in zip(encs, decs, saved):
+            out = dec.out.view(enc.B, e, enc.pitch)
+            for b in range(enc.B):
+                for i, j in enumerate(dec.err_host[b]):
+                    assert torch.equal(out[b, i, :L], sv[(b, int(j))]), (enc.B, b, i)
+    finally:
+        ctx.set_decode_kernel("auto")
+
+
+def test_bench_c4_two_ranks_ragged():
+    """`bench.py --gpus 2 --config c4` (two ranks on device 0, gloo): 2501
+    blocks do not divide by two -- rank 0 streams 1251 and rank 1 1250,
+    both in ragged batches, every batch verified; the shares are contiguous
+    and cover every block once."""
+    line = run_bench(["--gpus", "2", "--same-device", "--dist-backend", "gloo", "--config", "c4",
+                      "--blocks", "2501", "--batch", "512", "--warmup", "1", "--no-cpu-baseline"])
+    assert line["n_gpus"] == 2 and line["verified"]
+    assert line["streamed"]["mismatch_bytes"] == 0 and line["streamed"]["blocks_total"] == 2501
+    ranks = sorted(line["ranks"], key=lambda r: r["rank"])
+    assert [(r["block0"], r["blocks"], r["batches"]) for r in ranks] == [(0, 1251, 3), (1251, 1250, 3)]
+
+
+def test_bench_c5_two_ranks():
+    """`bench.py --gpus 2 --config c5` (the 8-GPU wide-stripe config, here
+    two ranks on device 0 with 3 blocks each): disjoint shards, erasure lists
+    by global block index, verified."""
+    line = run_bench(["--gpus", "2", "--same-device", "--dist-backend", "gloo", "--config", "c5",
+                      "--blocks", "3", "--steps", "2", "--warmup", "1", "--no-cpu-baseline"])
+    assert line["n_gpus"] == 2 and line["verified"]
+    assert line["config"]["symbols"] == 100 and line["config"]["erased"] == 20
+    ranks = sorted(line["ranks"], key=lambda r: r["rank"])
+    assert [(r["block0"], r["blocks"]) for r in ranks] == [(0, 3), (3, 3)]
+    for r in ranks:
+        err = rsgpu.erasure_patterns(1, r["block0"], r["blocks"], 100, 20)
+        assert r["err_sha"] == hashlib.sha256(err.tobytes()).hexdigest()
+
+
+def test_cpp_runner_threads_share_a_gpu(tmp_path):
+    """rs_throughput --gpus 2 --same-device: two host threads, each owning
+    its own rsgpu_ctx on device 0, run encode and decode at the same time
+    (every timed region starts on a barrier) -- the thread-safety promise of
+    include/rsgpu.h for distinct contexts.  Every decode is verified (a
+    rejected measurement fails the run) and the job row counts both GPUs'
+    bytes."""
+    runner = os.path.join(BIN, "rs_throughput")
+    csv_path = tmp_path / "mt.csv"
+    r = subprocess.run([runner, "--gpus", "2", "--same-device", "--symbols", "64", "16",
+                        "--symbol_size", "1000000", "--loss_rate", "0.5", "--blocks", "3", "--runs", "2",
+                        "--csv_file", str(csv_path)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    lines = csv_path.read_text().strip().splitlines()
+    head = lines[0].split(",")
+    assert head[-5:] == ["gpus", "resident", "run", "seconds", "goodput"]
+    assert len(lines) == 1 + 2 * 2 * 2
+    for ln in lines[1:]:
+        f = dict(zip(head, ln.split(",")))
+        assert f["gpus"] == "2" and f["resident"] == "device" and float(f["goodput"]) > 0
+
+
+@pytest.mark.parametrize("extra", [[], ["--gpus", "2", "--same-device"]])
+def test_cpp_runner_host_resident(extra):
+    """rs_throughput --resident host: the blocks live in pinned host memory as
+    the reference's do; encode_all / decode_all carry the copies (the
+    library's chunked three-stream pipeline), the recovered rows are compared
+    on the host.  Short rows (whole-block copies) and long rows (survivor
+    runs), one and two threads."""
+    runner = os.path.join(BIN, "rs_throughput")
+    r = subprocess.run([runner, "--resident", "host", "--symbols", "64", "16", "--symbol_size", "1000000",
+                        "32000", "--loss_rate", "0.5", "--blocks", "3"] + extra,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert r.stdout.count("resident=host") == 2 * 2 * 2, r.stdout
+
+
+@pytest.mark.parametrize("k,e,L,B", [(64, 32, 1000000, 3), (16, 4, 1000000, 2), (64, 32, 32000, 100),
+                                     (20, 7, 4096, 5), (10, 4, 1000, 3)])
+def test_host_resident_api_poisoned(ctx, orc, k, e, L, B):
+    """rsgpu_encode_blocks_host / rsgpu_decode_blocks_host on pinned host rows
+    with a host pitch of exactly L (the reference's rows; device rows are
+    re-pitched): parity equals the device path's, and the decode recovers the
+    originals while every erased row in HOST memory holds 0xA5 (only
+    survivors and parity may cross the link and be read).  A small block is
+    compared with the oracle too."""
+    enc = rsgpu.GpuEncoder(k, L, e, blocks=B, seed=53, ctx=ctx)
+    enc.encode_all()
+    dec = rsgpu.GpuDecoder(k, L, e, blocks=B, seed=53, ctx=ctx)
+    torch.cuda.synchronize()
+    src_d = enc.src.view(B, k, enc.pitch)[:, :, :L]
+    h_src = torch.empty((B, k, L), dtype=torch.uint8, pin_memory=True)
+    h_src.copy_(src_d)
+    h_par = torch.empty((B, e, L), dtype=torch.uint8, pin_memory=True)
+    ctx.encode_blocks_host(k, e, L, L, B, h_src, h_par)
+    par_d = enc.par.view(B, e, enc.pitch)[:, :, :L].cpu()
+    assert torch.equal(h_par, par_d)
+    keep = h_src.clone()
+    for b in range(B):
+        for j in dec.err_host[b]:
+            h_src[b, int(j)] = 0xA5
+    h_out = torch.empty((B, e, L), dtype=torch.uint8, pin_memory=True)
+    h_st = np.full(B, -7, np.int32)
+    err = np.ascontiguousarray(dec.err_host)
+    ctx.decode_blocks_host(k, e, L, L, B, h_src, h_par, err, h_out, h_st)
+    assert (h_st == 0).all()
+    for b in range(B):
+        for i, j in enumerate(dec.err_host[b]):
+            assert torch.equal(h_out[b, i], keep[b, int(j)]), (b, i)
+    data = [keep[0, j].numpy() for j in range(k)]
+    rc, rec = orc.decode_block(data, [h_par[0, i].numpy() for i in range(e)], dec.err_host[0])
+    assert rc == 0 and all((h_out[0, i].numpy() == rec[i]).all() for i in range(e))

@@ -315,11 +315,11 @@ def test_plugin_dropin_reference_shape():
     assert r.stdout.count("complete=1 verified=1") == 6, r.stdout
 
 
-@pytest.mark.parametrize("mode", ["fused", "one_matrix", "general"])
+@pytest.mark.parametrize("mode", ["generated", "one_matrix", "general"])
 def test_decode_modes_end_to_end(mode):
     """Every decode kernel choice (rsgpu_set_decode_kernel): the one-matrix
-    k_rs_tc decode (default), the fused syndrome + solve kernel and the
-    general k x k inversion, through the reference-shaped plugin with device
+    k_rs_tc decode, the per-block generated code and the general k x k
+    inversion, through the reference-shaped plugin with device
     verification of every recovered byte."""
     import subprocess
     exe = os.path.join(os.path.dirname(HERE), "storage-benchmarks_amd", "bin", "plugin_dropin_test")
@@ -442,13 +442,14 @@ def test_ec_encode_data_row_passes(ctx, orc, length, per):
 
 
 def test_host_io_ragged_chunks(ctx):
-    """bench.host_io_pipelined (the overlapped PCIe-inclusive path): 6 blocks
-    in chunks of 4 (a ragged last chunk), survivors shipped as row runs; the
-    recovered rows on the device equal the originals and the host copies
-    equal the device rows.  The serial host_io_rate ships the same bytes."""
+    """bench.host_io_pipelined (the library's host-resident calls): 70 C4-shaped
+    blocks go through device staging in chunks (42 blocks of (64, 32, 32000)
+    per chunk: a ragged last chunk); the recovered rows that came back equal
+    the originals and the parity equals the device path's.  The serial
+    host_io_rate verifies too."""
     sys.path.insert(0, os.path.dirname(HERE))
     import bench
-    r = bench.host_io_pipelined(rsgpu, ctx, 16, 8, 64000, 6, seed=3, chunk=4, reps=1)
-    assert r["verified"] and r["blocks"] == 6
+    r = bench.host_io_pipelined(rsgpu, ctx, 64, 32, 32000, 70, seed=3, reps=1)
+    assert r["verified"] and r["blocks"] == 70
     s = bench.host_io_rate(rsgpu, ctx, 16, 8, 64000, 6, seed=3, reps=1)
     assert s["verified"] and s["poisoned"]

@@ -1,15 +1,69 @@
 // jit_profile.hip -- where the waves of k_rs_jit spend their time (tool, not
-// product).  Compiles the kernel source with -DRSGPU_JIT_PROF (per-wave
-// s_memtime sums per phase), writes random-coefficient code for every block
-// with the host emitters of rs_jit.h, copies it into executable device
-// memory, runs the decode kernel on synthetic rows and prints the average
-// cycles per wave in each phase.
+// product).  Instantiates the product kernel with its own hooks policy
+// (ProfHooks below: per-wave s_memtime sums per phase, and timing-only
+// variants that run other code than the block's own), writes
+// random-coefficient code for every block with the host emitters of rs_jit.h,
+// copies it into executable device memory, runs the decode kernel on
+// synthetic rows and prints the average cycles per wave in each phase.
 //   make -C storage-benchmarks_amd build/tc_handlers.inc
-//   hipcc --offload-arch=gfx950 -O3 -std=c++20 -DRSGPU_JIT_PROF \
+//   hipcc --offload-arch=gfx950 -O3 -std=c++20 \
 //     -Istorage-benchmarks_amd/csrc -Istorage-benchmarks_amd/build \
 //     -o tools/jit_profile tools/jit_profile.hip -lhsa-runtime64
-//   tools/jit_profile [blocks=512] [k=64] [rows=32]
+//   tools/jit_profile [blocks=512] [k=64] [rows=32] [extra_lds] [mac_order] [xcd]
+//                     [share=0|1|2] [inv=1|0]
+//   share 1: every wave runs wave 0's code, 2: block 0's too; inv 0: no
+//   s_icache_inv (both timing only: wrong results)
 #include "../storage-benchmarks_amd/csrc/rs_jit.hip"
+
+namespace jitprof {
+__device__ unsigned long long rsgpu_jit_prof[8];
+
+template <int SHARE, bool INV>
+struct ProfHooks {
+    struct Timer {
+        unsigned long long sum[8] = {}, t, start;
+        __device__ Timer() : t(__builtin_amdgcn_s_memtime()), start(t) {}
+        __device__ void mark(int p)
+        {
+            const unsigned long long n = __builtin_amdgcn_s_memtime();
+            sum[p] += n - t;
+            t = n;
+        }
+        __device__ void end(int lane)
+        {
+            sum[7] = __builtin_amdgcn_s_memtime() - start;
+            if (lane == 0 && (blockIdx.x & 63) == 0)
+                for (int i = 0; i < 8; ++i)
+                    atomicAdd(&rsgpu_jit_prof[i], sum[i]);
+        }
+    };
+    static constexpr bool kInvalidate = INV;
+    __device__ static const uint8_t* code(const rsgpu::JitArgs& a, bool shared, int b, int wave, int nch)
+    {
+        if (SHARE == 0)
+            return rsgpu::jitk::JitHooks::code(a, shared, b, wave, nch);
+        return a.code + (size_t)(SHARE == 2 ? 0 : b) * a.block_stride;
+    }
+};
+
+template <int NW, int SHARE, bool INV>
+void launch(const rsgpu::JitArgs& a, int B, int extra_lds)
+{
+    hipLaunchKernelGGL((rsgpu::jitk::k_rs_jit<NW, false, ProfHooks<SHARE, INV>>),
+                       dim3((unsigned)((a.len + 2047) / 2048), (unsigned)B), dim3(64 * NW), extra_lds, 0, a);
+}
+
+template <int NW>
+void launch_mode(const rsgpu::JitArgs& a, int B, int extra_lds, int share, bool inv)
+{
+    if (share == 1)
+        inv ? launch<NW, 1, true>(a, B, extra_lds) : launch<NW, 1, false>(a, B, extra_lds);
+    else if (share == 2)
+        inv ? launch<NW, 2, true>(a, B, extra_lds) : launch<NW, 2, false>(a, B, extra_lds);
+    else
+        inv ? launch<NW, 0, true>(a, B, extra_lds) : launch<NW, 0, false>(a, B, extra_lds);
+}
+}  // namespace jitprof
 
 #include <hsa/hsa.h>
 #include <hsa/hsa_ext_amd.h>
@@ -64,6 +118,8 @@ int main(int argc, char** argv)
     // registers, 2 = by (H, L)
     const int mac_order = argc > 5 ? atoi(argv[5]) : 0;
     const int xcd = argc > 6 ? atoi(argv[6]) : 0;  // XCD-contiguous (block, tile) order
+    const int share = argc > 7 ? atoi(argv[7]) : 0;
+    const bool inv = argc > 8 ? atoi(argv[8]) != 0 : true;
     const long long L = 1000000, pitch = 1000192;
     uint8_t* rows;
     if (hipMalloc(&rows, (size_t)B * (k + e) * pitch) != hipSuccess) {
@@ -159,16 +215,17 @@ int main(int argc, char** argv)
     a.xcd_order = xcd;
     for (int rep = 0; rep < 4; ++rep) {  // warm, then measured
         unsigned long long z[8] = {};
-        (void)hipMemcpyToSymbol(HIP_SYMBOL(jitk::rsgpu_jit_prof), z, sizeof z);
+        (void)hipMemcpyToSymbol(HIP_SYMBOL(jitprof::rsgpu_jit_prof), z, sizeof z);
         hipEvent_t e0, e1;
         (void)hipEventCreate(&e0);
         (void)hipEventCreate(&e1);
         (void)hipEventRecord(e0);
-        if (extra_lds && e > 24)
-            hipLaunchKernelGGL((jitk::k_rs_jit<4, false>), dim3((unsigned)((L + 2047) / 2048), (unsigned)B), dim3(256),
-                               extra_lds, 0, a);
-        else
-            (void)launch_rs_jit(a, B, 0);
+        switch (NW) {
+        case 1: jitprof::launch_mode<1>(a, B, extra_lds, share, inv); break;
+        case 2: jitprof::launch_mode<2>(a, B, extra_lds, share, inv); break;
+        case 3: jitprof::launch_mode<3>(a, B, extra_lds, share, inv); break;
+        default: jitprof::launch_mode<4>(a, B, extra_lds, share, inv); break;
+        }
         (void)hipEventRecord(e1);
         if (hipDeviceSynchronize() != hipSuccess) {
             printf("kernel failed\n");
@@ -177,7 +234,7 @@ int main(int argc, char** argv)
         float ms = 0;
         (void)hipEventElapsedTime(&ms, e0, e1);
         unsigned long long p[8];
-        (void)hipMemcpyFromSymbol(p, HIP_SYMBOL(jitk::rsgpu_jit_prof), sizeof p);
+        (void)hipMemcpyFromSymbol(p, HIP_SYMBOL(jitprof::rsgpu_jit_prof), sizeof p);
         const double waves = (double)p[7] > 0 ? 1 : 1;
         (void)waves;
         const char* names[8] = {"wait vmcnt (LDS-DMA)", "transpose in", "barrier",

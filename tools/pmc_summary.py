@@ -11,7 +11,7 @@ def short(k: str) -> str:
         return "k_rs_jit%s(decode)" % ("16" if "Wide<16" in k else "12" if "Wide<12" in k else "10")
     if "k_rs_jit" in k:  # <NW, true>: the shared-program encode
         return "k_rs_jit(encode)" if "true>" in k.split("(")[0] else "k_rs_jit(decode)"
-    for key in ("k_rs_decode_fused", "k_rs_tc", "k_rs_jit", "k_rs_bs", "k_dot_generic",
+    for key in ("k_rs_tc", "k_rs_jit", "k_rs_bs", "k_dot_generic",
                 "k_decode_prepare_syn", "k_fill_synth"):
         if key in k:
             return key

@@ -16,8 +16,6 @@ from collections import defaultdict
 def name_of(kernel: str) -> str:
     if "k_rs_bs<" in kernel:
         return "k_rs_bs(syndrome)" if kernel.split(">")[0].rstrip().endswith("true") else "k_rs_bs(encode)"
-    if "k_rs_decode_fused" in kernel:
-        return "k_rs_decode_fused"
     if "k_rs_jitw" in kernel:  # rs_jit.h Wide<R, CS>
         return "k_rs_jit%s(decode)" % ("16" if "Wide<16" in kernel else "12" if "Wide<12" in kernel else "10")
     if "k_rs_jit" in kernel:

@@ -1,12 +1,46 @@
 // tc_profile.hip -- where the waves of k_rs_tc spend their time (tool, not
-// product).  Compiles the kernel source with -DRSGPU_TC_PROF (per-wave
-// s_memtime sums per phase), runs it on synthetic rows with random
+// product).  Instantiates the product kernel with a hooks policy whose Timer
+// sums s_memtime per phase, runs it on synthetic rows with random
 // coefficients, and prints the average cycles per wave in each phase.
 //   make -C storage-benchmarks_amd build/tc_handlers.inc
-//   hipcc --offload-arch=gfx950 -O3 -std=c++20 -DRSGPU_TC_PROF \
+//   hipcc --offload-arch=gfx950 -O3 -std=c++20 \
 //     -Istorage-benchmarks_amd/csrc -Istorage-benchmarks_amd/build \
 //     -o tools/tc_profile tools/tc_profile.hip
 #include "../storage-benchmarks_amd/csrc/rs_tc.hip"
+
+namespace tcprof {
+__device__ unsigned long long rsgpu_tc_prof[8];
+struct ProfHooks {
+    struct Timer {
+        unsigned long long sum[8] = {}, t, start;
+        __device__ Timer() : t(__builtin_amdgcn_s_memtime()), start(t) {}
+        __device__ void mark(int p)
+        {
+            const unsigned long long n = __builtin_amdgcn_s_memtime();
+            sum[p] += n - t;
+            t = n;
+        }
+        __device__ void end(int lane)
+        {
+            sum[7] = __builtin_amdgcn_s_memtime() - start;
+            if (lane == 0 && (blockIdx.x & 63) == 0)  // sampled: same-address atomics serialise
+                for (int i = 0; i < 8; ++i)
+                    atomicAdd(&rsgpu_tc_prof[i], sum[i]);
+        }
+    };
+};
+void launch(const rsgpu::TcArgs& a, int B)
+{
+    const int nw = rsgpu::tc_rows_per_pass(a.rows) / 8;
+    dim3 grid((unsigned)((a.len + 2047) / 2048), (unsigned)B);
+    switch (nw) {
+    case 1: hipLaunchKernelGGL((rsgpu::tc::k_rs_tc<1, ProfHooks>), grid, dim3(64), 0, 0, a, 1); break;
+    case 2: hipLaunchKernelGGL((rsgpu::tc::k_rs_tc<2, ProfHooks>), grid, dim3(128), 0, 0, a, 1); break;
+    case 3: hipLaunchKernelGGL((rsgpu::tc::k_rs_tc<3, ProfHooks>), grid, dim3(192), 0, 0, a, 1); break;
+    default: hipLaunchKernelGGL((rsgpu::tc::k_rs_tc<4, ProfHooks>), grid, dim3(256), 0, 0, a, 1); break;
+    }
+}
+}  // namespace tcprof
 
 #include <cstdio>
 #include <vector>
@@ -58,24 +92,25 @@ int main(int argc, char** argv)
     a.addr = d_addr;
     a.k = k;
     a.rows = nrows;
+    a.dst_stride = k;  // block b writes its own rows (dsts == srcs)
     a.addr_stride = (long long)k * slots;
     a.len = L;
     a.status = nullptr;
     for (int i = 0; i < 2; ++i)
-        (void)launch_rs_tc(a, B, 0);
+        tcprof::launch(a, B);
     unsigned long long zero[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    (void)hipMemcpyToSymbol(HIP_SYMBOL(tc::rsgpu_tc_prof), zero, sizeof zero);
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(tcprof::rsgpu_tc_prof), zero, sizeof zero);
     hipEvent_t e0, e1;
     (void)hipEventCreate(&e0);
     (void)hipEventCreate(&e1);
     (void)hipEventRecord(e0);
-    (void)launch_rs_tc(a, B, 0);
+    tcprof::launch(a, B);
     (void)hipEventRecord(e1);
     (void)hipEventSynchronize(e1);
     float ms;
     (void)hipEventElapsedTime(&ms, e0, e1);
     unsigned long long prof[8];
-    (void)hipMemcpyFromSymbol(prof, HIP_SYMBOL(tc::rsgpu_tc_prof), sizeof prof);
+    (void)hipMemcpyFromSymbol(prof, HIP_SYMBOL(tcprof::rsgpu_tc_prof), sizeof prof);
     const double waves = (double)(((L + 2047) / 2048 + 63) / 64) * B * (slots / 8);  // sampled WGs
     // one barrier per step: phase 0 is the wait, phase 1 empty, phase 3 the barrier plus the next issue
     const char* names[8] = {"wait vmcnt", "-", "transpose in", "barrier + issue DMA",
