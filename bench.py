@@ -85,6 +85,8 @@ def parse(argv=None):
     p.add_argument("--sq-counters", default=os.path.join(ROOT, "profiles", "r02_sq_counters.txt"),
                    help="SQ counter summary of the same workload (tools/pmc_sq.sh + "
                         "tools/pmc_summary.py): VALU-issue roofline of each kernel")
+    p.add_argument("--valu-ceiling", default=os.path.join(ROOT, "profiles", "r03_valu_ceiling.json"),
+                   help="measured VALU issue ceiling (tools/ubench_issue + tools/valu_ceiling.py)")
     # testing the N-rank path on a one-GPU box: every rank on device 0, gloo
     # for the barrier / max-time reduction (RCCL needs one GPU per rank)
     p.add_argument("--same-device", action="store_true", help=argparse.SUPPRESS)
@@ -384,10 +386,13 @@ def kernel_stats(recs, steps, alg):
     return per, kernels
 
 
-# SIMD cycles per wave64 v_bitop3 / v_xor with >= 4 waves per SIMD
-# (tools/ubench_bank.hip, profiles/r02_ubench_bank.log): the VALU issue limit
-VALU_CYCLES_PER_INST = 2.6
+# The VALU issue ceiling, in SIMD cycles per wave64 instruction: the chip
+# guide's 2 (SIMD-32: a wave64 VALU issues over 2 cycles, MI355X_MICROARCH.md)
+# and the ceiling measured for v_bitop3 on random data with tools/ubench_issue
+# (GRBM_GUI_ACTIVE and SQ_INSTS_VALU from ONE counter pass, no wall clock)
+GUIDE_CYCLES_PER_VALU = 2.0
 SIMDS = 1024  # 256 CUs x 4
+XCDS = 8
 
 
 def sq_counters(path):
@@ -403,19 +408,31 @@ def sq_counters(path):
     return out
 
 
-def valu_roofline(counters, kernel, avg_ms):
-    """VALU-issue roofline of one kernel launch: the time its VALU
-    instructions need at the issue limit, at the clock the launch ran at
-    (GRBM_GUI_ACTIVE over 8 XCDs), against its measured time."""
+def valu_roofline(counters, kernel, ceiling):
+    """How close one kernel's VALU stream runs to the issue ceiling, from
+    counters of ONE pass only (time-independent): SIMD-cycles per wave64
+    VALU = (GRBM_GUI_ACTIVE / 8 XCDs) * 1024 SIMDs / SQ_INSTS_VALU, against
+    the guide's 2 cycles and against the measured ceiling `ceiling`."""
     c = counters.get(kernel) or counters.get(kernel.split("(")[0])
     if not c or "SQ_INSTS_VALU" not in c or "GRBM_GUI_ACTIVE" not in c:
         return None
-    ghz = c["GRBM_GUI_ACTIVE"] / 8 / (avg_ms * 1e-3) / 1e9
-    need_ms = c["SQ_INSTS_VALU"] * VALU_CYCLES_PER_INST / SIMDS / (ghz * 1e9) * 1e3
-    return {"valu_insts_per_launch": c["SQ_INSTS_VALU"],
-            "valu_insts_per_wave": round(c["SQ_INSTS_VALU"] / c["SQ_WAVES"], 1) if c.get("SQ_WAVES") else None,
-            "clock_ghz": round(ghz, 3), "cycles_per_inst": VALU_CYCLES_PER_INST,
-            "issue_bound_ms": round(need_ms, 3), "frac": round(need_ms / avg_ms, 4)}
+    cpi = c["GRBM_GUI_ACTIVE"] / XCDS * SIMDS / c["SQ_INSTS_VALU"]
+    out = {"valu_insts_per_launch": c["SQ_INSTS_VALU"],
+           "valu_insts_per_wave": round(c["SQ_INSTS_VALU"] / c["SQ_WAVES"], 1) if c.get("SQ_WAVES") else None,
+           "simd_cycles_per_valu": round(cpi, 3),
+           "frac_of_guide_2cycle": round(GUIDE_CYCLES_PER_VALU / cpi, 4)}
+    if ceiling:
+        out["measured_ceiling_cycles_per_valu"] = ceiling
+        out["frac_of_measured_ceiling"] = round(ceiling / cpi, 4)
+    return out
+
+
+def valu_ceiling(path):
+    """Measured issue ceiling (SIMD cycles per VALU) at 4 waves per SIMD, or None."""
+    try:
+        return json.load(open(path))["waves_per_simd_4"]["simd_cycles_per_valu"]
+    except (OSError, KeyError, ValueError):
+        return None
 
 
 def hbm_probe(dev, mib=2048, reps=5):
@@ -703,7 +720,8 @@ def main(argv=None):
     if (args.sq_counters and os.path.exists(args.sq_counters) and args.config == "c3"
             and not args.blocks and not custom):
         sq = sq_counters(args.sq_counters)
-        valu = {kn: r for kn in per if (r := valu_roofline(sq, kn, per[kn][0] / per[kn][1]))}
+        ceil = valu_ceiling(args.valu_ceiling)
+        valu = {kn: r for kn in per if (r := valu_roofline(sq, kn, ceil))}
     op_bytes = float((k + e) * L) * (out_bytes_step / (2.0 * e * L))
     step_frac = (2 * op_bytes) / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBPS
 
@@ -728,10 +746,12 @@ def main(argv=None):
                      # north_star's HBM-read variant: only the k source rows read
                      # per block count
                      "frac_read": round(read_bytes / (dom_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
-                     # what bounds the kernels instead: VALU issue at the
-                     # power-limited clock (SQ counters of the same workload)
+                     # how close each kernel's VALU stream runs to issue
+                     # (SQ counters of the same workload, one pass)
                      "valu": valu,
-                     "valu_source": (os.path.relpath(args.sq_counters, ROOT) if valu else None)},
+                     "valu_source": (os.path.relpath(args.sq_counters, ROOT) if valu else None),
+                     "valu_ceiling_source": (os.path.relpath(args.valu_ceiling, ROOT)
+                                             if valu and valu_ceiling(args.valu_ceiling) else None)},
         "cpu_baseline": None,
     }
     line.update(extra)

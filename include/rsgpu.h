@@ -150,7 +150,10 @@ size_t rsgpu_decode_workspace_bytes(int k, int e, size_t blocks);
  *               (len > 94 KiB) and the call has >= 4096 (block, tile)
  *               pairs, else ONE_MATRIX (the default)
  *   ONE_MATRIX  closed-form e x k decode rows V_E^-1 [V_kept | I] (e <= 32),
- *               one threaded-code pass over the k - e survivors + e parity
+ *               one threaded-code pass over the k - e survivors + e parity;
+ *               rsgpu_decode_blocks runs a small call (< 2048 (block, 2 KB
+ *               column) pairs, e <= 8, k <= 64) as ONE launch that builds the
+ *               rows itself (the prepare/apply pair keeps two)
  *   GENERAL     the reference's k x k survivor-matrix inversion on the
  *               device (isa.cpp:177-204), then the decode rows; any e
  *   GENERATED   the ONE_MATRIX rows baked into per-block straight-line code

@@ -147,6 +147,26 @@ LDS_T = 2048     # LDS bytes per source: [2 halves][64 lanes] x 16 B
 LDS_H = 1024
 
 
+def chunk_v(nt: int) -> list:
+    """chunk(nt) for nt <= 4 with the handler addresses taken from a VGPR
+    instead of a scalar load (k_rs_tc_fused, which computes them itself):
+    lane 16 t + i of %[av] holds dword i of source t's 8 addresses, moved into
+    the source's SGPR bank by v_readlane_b32 where chunk() issues its
+    s_load_dwordx16 (at least the 22 composites before the first use)."""
+    assert 1 <= nt <= 4
+    ins = chunk(nt)
+    out = []
+    for x in ins:
+        if x.startswith("s_load_dwordx16"):
+            bank = int(x.split("s[")[1].split(":")[0])
+            off = x.rsplit(",", 1)[1].strip()
+            t = 0 if off == "0" else int(off[3:-1])  # %[oN] -> N
+            out += [f"v_readlane_b32 s{bank + i}, %[av], {16 * t + i}" for i in range(16)]
+        else:
+            out.append(x)
+    return out
+
+
 def chunk(nt: int) -> list:
     """One LDS chunk of nt sources in one asm statement (rs_tc.hip): every
     asynchronous load it issues is also waited for inside it.  Per source t:
@@ -224,6 +244,11 @@ def main() -> None:
     for nt in range(1, C + 1):
         lines.append(f"#define RSGPU_TC_CHUNK{nt} \\")
         for i in chunk(nt):
+            lines.append(f'    "{i}\\n" \\')
+        lines.append("")
+    for nt in range(1, 5):
+        lines.append(f"#define RSGPU_TC_CHUNKV{nt} \\")
+        for i in chunk_v(nt):
             lines.append(f'    "{i}\\n" \\')
         lines.append("")
     lines.append(f"#define RSGPU_TC_C {C}")

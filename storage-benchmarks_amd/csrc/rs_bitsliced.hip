@@ -99,11 +99,11 @@ __device__ __forceinline__ void prog_op(uint32_t (&V)[NV])
 
 // Output O of source T: its one or two values; source 0's single plane
 // moves to the partner source of T0Pair (one 3-input XOR for both terms)
-template <class PR, class PP, int T, int O, int NV>
+template <class PR, class PP, bool PAIR, int T, int O, int NV>
 __device__ __forceinline__ void prog_out(uint32_t& acc, const uint32_t (&V)[NV], const uint32_t (&p0)[8])
 {
     constexpr int x = PR::outs[O][0], y = PR::outs[O][1];
-    constexpr int partner = PP::partner[O];
+    constexpr int partner = PAIR ? PP::partner[O] : 0;  // 0: source 0 adds its own plane
     if constexpr (T == 0 && partner != 0) {
         // added by source `partner`
     } else if constexpr (T != 0 && partner == T) {
@@ -119,7 +119,7 @@ __device__ __forceinline__ void prog_out(uint32_t& acc, const uint32_t (&V)[NV],
 // consume source T of the chunk from planes p (all lanes), for this wave's
 // rows: the generated program's composites, then one XOR per output plane
 // (p0: the chunk's source 0 planes, for the outputs paired with it)
-template <class P, int R0, int NR, int T>
+template <class P, int R0, int NR, int T, bool PAIR = true>
 __device__ __forceinline__ void consume(uint32_t (&acc)[NR][8], const uint32_t (&p)[8], const uint32_t (&p0)[8])
 {
     using PR = EncProg<P::k, P::e, P::c, R0, NR, T>;
@@ -133,7 +133,7 @@ __device__ __forceinline__ void consume(uint32_t (&acc)[NR][8], const uint32_t (
         (prog_op<PR, Is>(V), ...);
     }(std::make_integer_sequence<int, PR::NOPS>{});
     [&]<int... Os>(std::integer_sequence<int, Os...>) {
-        (prog_out<PR, PP, T, Os>(acc[Os / 8][Os % 8], V, p0), ...);
+        (prog_out<PR, PP, PAIR, T, Os>(acc[Os / 8][Os % 8], V, p0), ...);
     }(std::make_integer_sequence<int, NR * 8>{});
 }
 
@@ -301,6 +301,86 @@ __global__ __launch_bounds__(64 * NW, (bs_waves_per_simd<E, NW>())) void k_rs_bs
     }(std::make_integer_sequence<int, NW>{});
 }
 
+// Small batches of a single-chunk code (C == K, E <= 8; C2: one block of
+// (16, 4, 1e6), 489 tiles, where one wave per tile leaves most SIMDs idle
+// and walks all K sources in series): SPL waves split a tile's sources,
+// wave w taking T = w, w + SPL, ... with the compile-time programs of those
+// T (no source 0 pairing: the partner may belong to another wave), straight
+// from global memory into registers; the partial accumulators meet in LDS
+// and wave w finishes rows w, w + SPL, ...
+template <int K, int E, int SPL, int G>
+__device__ __forceinline__ void split_group(const Args& a, uint32_t (&acc)[E][8], long long loff)
+{
+    using P = PlanHolder<K, E, K>;
+    const uint8_t* sb = a.src + (size_t)blockIdx.y * K * a.pitch;
+    constexpr int NT = (K - G + SPL - 1) / SPL;  // this wave's sources
+    uint32_t W[NT][8];
+#pragma unroll
+    for (int i = 0; i < NT; ++i)  // every load in flight before the first use
+        load32(sb + (size_t)(G + SPL * i) * a.pitch, loff, true, W[i]);
+    const uint32_t m4 = vconst(0x0F0F0F0Fu), m2 = vconst(0x33333333u), m1 = vconst(0x55555555u);
+    const uint32_t none[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    [&]<int... Is>(std::integer_sequence<int, Is...>) {
+        (
+            [&] {
+                tr8(W[Is], m4, m2, m1);
+                consume<P, 0, E, G + SPL * Is, false>(acc, W[Is], none);
+            }(),
+            ...);
+    }(std::make_integer_sequence<int, NT>{});
+}
+
+template <int K, int E, int SPL>
+__global__ __launch_bounds__(64 * SPL) void k_rs_bs_split(Args a)
+{
+    static_assert(E <= 8 && K >= SPL, "split encode: one row group, every wave a source");
+    __shared__ uint32_t part[SPL][E * 8][64];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const long long off = (long long)blockIdx.x * 2048 + lane * 32;
+    const bool inb = off + 32 <= a.len;
+    const long long loff = inb ? off : 0;  // out-of-range lanes re-read the row head
+    uint32_t acc[E][8];
+#pragma unroll
+    for (int r = 0; r < E; ++r)
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+            acc[r][q] = 0;
+    [&]<int... Gs>(std::integer_sequence<int, Gs...>) {
+        ((wave == Gs ? split_group<K, E, SPL, Gs>(a, acc, loff) : void()), ...);
+    }(std::make_integer_sequence<int, SPL>{});
+#pragma unroll
+    for (int r = 0; r < E; ++r)
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+            part[wave][r * 8 + q][lane] = acc[r][q];
+    __syncthreads();
+    if (!inb)
+        return;
+    const uint32_t m4 = vconst(0x0F0F0F0Fu), m2 = vconst(0x33333333u), m1 = vconst(0x55555555u);
+    uint8_t* ob = a.out + (size_t)blockIdx.y * E * a.pitch;
+    for (int r = wave; r < E; r += SPL) {
+        uint32_t W[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+        for (int w = 0; w < SPL; ++w)
+#pragma unroll
+            for (int q = 0; q < 8; ++q)
+                W[q] ^= part[w][r * 8 + q][lane];
+        tr8(W, m4, m2, m1);
+        store32(ob + (size_t)r * a.pitch, off, W);
+    }
+}
+
+template <int K, int E>
+hipError_t launch_split(const uint8_t* src, uint8_t* out, long long pitch, long long len, long long blocks,
+                        hipStream_t st)
+{
+    Args a{src, out, pitch, len};
+    dim3 grid((unsigned)((len + 2047) / 2048), (unsigned)blocks);
+    hipLaunchKernelGGL((k_rs_bs_split<K, E, 4>), grid, dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+
 template <int K, int E, int C, int NW>
 hipError_t launch(const uint8_t* src, uint8_t* out, long long pitch, long long len,
                   long long blocks, hipStream_t st)
@@ -318,6 +398,21 @@ bool rs_bitsliced_available(int k, int e)
     return (k == 16 && e == 4) || (k == 16 && e == 8) || (k == 64 && e == 32) ||
            (k == 100 && e == 20) || (k == 5 && e == 4) || (k == 20 && e == 7) ||
            (k == 64 && e == 16);
+}
+
+bool rs_bitsliced_split_available(int k, int e)
+{
+    return (k == 16 && e == 4) || (k == 16 && e == 8) || (k == 5 && e == 4) || (k == 20 && e == 7);
+}
+
+hipError_t launch_rs_bitsliced_split(int k, int e, const uint8_t* src, uint8_t* out, long long pitch,
+                                     long long len, long long blocks, hipStream_t st)
+{
+    if (k == 16 && e == 4) return bs::launch_split<16, 4>(src, out, pitch, len, blocks, st);
+    if (k == 16 && e == 8) return bs::launch_split<16, 8>(src, out, pitch, len, blocks, st);
+    if (k == 5 && e == 4) return bs::launch_split<5, 4>(src, out, pitch, len, blocks, st);
+    if (k == 20 && e == 7) return bs::launch_split<20, 7>(src, out, pitch, len, blocks, st);
+    return hipErrorInvalidValue;
 }
 
 hipError_t launch_rs_bitsliced(int k, int e, const uint8_t* src, uint8_t* out, long long pitch,

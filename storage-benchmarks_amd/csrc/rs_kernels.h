@@ -67,6 +67,11 @@ hipError_t launch_compare_rows(const uint8_t* src, long long src_pitch, int k, c
 bool rs_bitsliced_available(int k, int e);
 hipError_t launch_rs_bitsliced(int k, int e, const uint8_t* src, uint8_t* out, long long pitch,
                                long long len, long long blocks, hipStream_t st);
+// Small batches of the single-chunk codes (16,4) (16,8) (5,4) (20,7): four
+// waves per tile split the sources (k_rs_bs_split), same bytes.
+bool rs_bitsliced_split_available(int k, int e);
+hipError_t launch_rs_bitsliced_split(int k, int e, const uint8_t* src, uint8_t* out, long long pitch,
+                                     long long len, long long blocks, hipStream_t st);
 
 // Closed-form decode prepare for the gf_gen_rs_matrix code with e erased
 // originals and all e parity rows surviving, per block: erasure list
@@ -164,6 +169,28 @@ int tc_handler_count();
 int tc_slot_copy(int slot);
 hipError_t tc_query_handlers(unsigned long long* d_out, hipStream_t st);
 hipError_t launch_rs_tc(const TcArgs& a, long long blocks, hipStream_t st);
+// The same for small batches with rows <= 8 (k >= 4): four waves per tile
+// split the sources, partial accumulators reduced in LDS (rs_tc.hip
+// k_rs_tc_split); addr [B][k][8] as above.
+hipError_t launch_rs_tc_split(const TcArgs& a, long long blocks, hipStream_t st);
+// The whole one-matrix decode of a small batch in one launch (rs_tc.hip
+// k_rs_tc_fused): e <= 8, 1 <= k <= 64, len % 32 == 0, 16-byte aligned rows;
+// the closed-form decode rows of every block built in the kernel, status
+// written per block (0, or -2 for a malformed erasure list).
+struct TcFusedArgs {
+    int k, e;
+    long long len, pitch, blocks;
+    const uint8_t* err;      // [B][e] erased originals, strictly ascending
+    const uint8_t* src;      // [B][k] rows (erased ones never read)
+    const uint8_t* par;      // [B][e] rows
+    uint8_t* out;            // [B][e] rows
+    int* status;             // [B]
+    // handler of (slot s, coefficient c): map_base + (map_copy[s] 256 + c) map_stride
+    unsigned long long map_base;
+    int map_stride;
+    int map_copy[8];
+};
+hipError_t launch_rs_tc_fused(const TcFusedArgs& a, hipStream_t st);
 
 hipError_t launch_row_ptrs(const uint8_t* base, long long pitch, int rows_per_block,
                            long long blocks, const uint8_t** out, hipStream_t st);

@@ -41,6 +41,7 @@
 #include <utility>
 
 #include "bitslice.h"
+#include "gf256.h"
 #include "rs_kernels.h"
 #include "tc_handlers.inc"
 
@@ -251,6 +252,277 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_num_vgpr(64))) void 
     tp.end(lane);
 }
 
+// Small batches, rows <= 8 (C2: one block of (16, 4, 1e6), 489 tiles): one
+// wave per tile would leave most SIMDs idle and walk all k sources in series
+// (13 us at C2).  Here SPL waves split a tile's sources: wave w takes the
+// contiguous range [w k / SPL, (w+1) k / SPL), loads it by LDS-DMA into its
+// own LDS part, transposes it and runs the same threaded code over it into
+// all rows (the address table [B][k][8] of tc_rows_per_pass(rows) = 8); then
+// the partial accumulators meet in LDS and wave w finishes rows w, w + SPL,
+// ...  No barrier until the reduction: each wave reads only its own part.
+template <int SPL>
+__global__ __launch_bounds__(64 * SPL) __attribute__((amdgpu_num_vgpr(64))) void k_rs_tc_split(TcArgs a)
+{
+    // per wave: C sources x [2 halves][64 lanes] x 16 B = 16 KiB, reused for
+    // the wave's partial accumulators (8 slots x 8 planes x 64 lanes x 4 B)
+    __shared__ uint4 lds[SPL][C * 2 * 64];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int b = blockIdx.y;
+    if (a.status && a.status[b] != 0)
+        return;
+    const int k = a.k;
+    const int j0 = wave * k / SPL, j1 = (wave + 1) * k / SPL;
+    const long long off = (long long)blockIdx.x * 2048 + lane * 32;
+    const uint32_t loff = off + 32 <= a.len ? (uint32_t)off : 0u;  // out-of-range lanes re-read the row head
+    const uint8_t* const* srcs = a.srcs + (size_t)b * k;
+    const unsigned long long* ap = a.addr + (size_t)b * a.addr_stride;
+    const uint32_t m4 = vconst(0x0F0F0F0Fu), m2 = vconst(0x33333333u), m1 = vconst(0x55555555u);
+    uint4* mine = lds[wave];
+    const uint32_t base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint4*)mine;
+    asm volatile(RSGPU_TC_ZERO ::: RSGPU_TC_ACC_CLOBBERS);
+    for (int c0 = j0; c0 < j1; c0 += C) {
+        const int nt = min(C, j1 - c0);
+        for (int t = 0; t < nt; ++t)
+            glds32(sload_ptr(srcs + c0 + t), loff, base + (uint32_t)(t * 2 * 64 * 16));
+        wait_vm(0);
+        for (int t = 0; t < nt; ++t) {
+            uint4 u = mine[(t * 2 + 0) * 64 + lane];
+            uint4 v = mine[(t * 2 + 1) * 64 + lane];
+            uint32_t W[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
+            tr8(W, m4, m2, m1);
+            mine[(t * 2 + 0) * 64 + lane] = make_uint4(W[0], W[1], W[2], W[3]);
+            mine[(t * 2 + 1) * 64 + lane] = make_uint4(W[4], W[5], W[6], W[7]);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        const uint32_t la = base + lane * 16;
+        const unsigned long long* pa = ap + (size_t)c0 * 8;
+#define RSGPU_TC_RUN(N)                                                                          \
+    asm volatile(RSGPU_TC_CHUNK##N                                                               \
+                 :                                                                               \
+                 : [la] "v"(la), [pa] "s"(pa), [o1] "i"(64), [o2] "i"(128), [o3] "i"(192),        \
+                   [o4] "i"(256), [o5] "i"(320), [o6] "i"(384), [o7] "i"(448)                     \
+                 : RSGPU_TC_CLOBBERS, RSGPU_TC_ACC_CLOBBERS, "memory")
+        switch (nt) {
+        case 1: RSGPU_TC_RUN(1); break;
+        case 2: RSGPU_TC_RUN(2); break;
+        case 3: RSGPU_TC_RUN(3); break;
+        case 4: RSGPU_TC_RUN(4); break;
+        case 5: RSGPU_TC_RUN(5); break;
+        case 6: RSGPU_TC_RUN(6); break;
+        case 7: RSGPU_TC_RUN(7); break;
+        default: RSGPU_TC_RUN(8); break;
+        }
+#undef RSGPU_TC_RUN
+    }
+    // partial accumulators -> this wave's part: [slot][plane][lane]
+    uint32_t* part = reinterpret_cast<uint32_t*>(mine);
+    [&]<int... Ss>(std::integer_sequence<int, Ss...>) {
+        (
+            [&] {
+                if (Ss < a.rows) {
+                    uint32_t W[8];
+                    read_slot<Ss>(W);
+#pragma unroll
+                    for (int q = 0; q < 8; ++q)
+                        part[(Ss * 8 + q) * 64 + lane] = W[q];
+                }
+            }(),
+            ...);
+    }(std::make_integer_sequence<int, 8>{});
+    __syncthreads();
+    if (off + 32 > a.len)
+        return;
+    uint8_t* const* dsts = a.dsts + (size_t)b * a.dst_stride;
+    for (int r = wave; r < a.rows; r += SPL) {
+        uint32_t W[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+        for (int w = 0; w < SPL; ++w) {
+            const uint32_t* pw = reinterpret_cast<const uint32_t*>(lds[w]);
+#pragma unroll
+            for (int q = 0; q < 8; ++q)
+                W[q] ^= pw[(r * 8 + q) * 64 + lane];
+        }
+        tr8(W, m4, m2, m1);
+        store32((uint8_t*)sload_ptr((const uint8_t* const*)(dsts + r)), off, W);
+    }
+}
+
+// The whole decode of a small batch in ONE launch (rsgpu_decode_blocks, C2:
+// one block of (16, 4, 1e6), e <= 8, k <= 64): every workgroup first builds
+// its block's e x k decode rows V_E^-1 [V_kept | I] in closed form (as
+// k_decode_prepare_syn, rs_kernels.hip: Lambda, w_i, Lambda(b_q), synthetic
+// division) with wave 0 and LDS tables, then runs k_rs_tc_split's work with
+// the handler addresses computed from the rows (handler of slot s for
+// coefficient c at map.base + (map.copy[s] 256 + c) map.stride) and handed
+// to the threaded code in a VGPR (RSGPU_TC_CHUNKV, v_readlane) instead of a
+// table in memory.  Saves the prepare launch and its table round trip.
+__device__ const GfTables kGfTc = make_gf_tables();
+
+template <int SPL>
+__global__ __launch_bounds__(64 * SPL) __attribute__((amdgpu_num_vgpr(64))) void k_rs_tc_fused(TcFusedArgs a)
+{
+    __shared__ uint4 lds[SPL][C * 2 * 64];  // per wave: its sources, then its partial rows
+    __shared__ uint8_t gexp[512], glog[256], coef[8 * 64], lv[64];
+    __shared__ uint8_t aa[8], lam[16], lws[8];
+    __shared__ int bad;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int b = blockIdx.y, k = a.k, e = a.e, nl = k - e;
+    for (int i = threadIdx.x; i < 512; i += 64 * SPL) {
+        gexp[i] = kGfTc.exp[i];
+        if (i < 256)
+            glog[i] = kGfTc.log[i];
+    }
+    __syncthreads();
+    if (wave == 0) {  // the whole wave runs every statement; lanes select what they write
+        auto gmul = [&](uint8_t x, uint8_t y) -> uint8_t { return (x && y) ? gexp[glog[x] + glog[y]] : (uint8_t)0; };
+        auto lds_sync = [] { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); };
+        const int j = lane < e ? a.err[(size_t)b * e + lane] : 255;  // lane i: erased original j_i
+        const int jp = __shfl_up(j, 1);
+        const bool badl = lane < e && (j >= k || (lane > 0 && j <= jp));  // strictly ascending, < k
+        const bool anybad = __ballot(badl) != 0;
+        if (lane == 0)
+            bad = anybad;
+        if (!anybad) {  // wave-uniform
+            if (lane < e)
+                aa[lane] = gexp[j];  // a_i = 2^(j_i)
+            lds_sync();
+            int below = 0;  // survivors, ascending
+            bool er = false;
+            for (int i = 0; i < e; ++i) {
+                const int ji = glog[aa[i]];
+                below += ji < lane;
+                er |= ji == lane;
+            }
+            if (lane < k && !er)
+                lv[lane - below] = (uint8_t)lane;
+            uint8_t lm = lane == 0 ? 1 : 0;  // Lambda(z) = prod (z + a_l): lane m, coefficient of z^m
+            for (int l = 0; l < e; ++l) {
+                const int prev = __shfl_up((int)lm, 1);
+                lm = (uint8_t)(lane == 0 ? 0 : prev) ^ gmul(aa[l], lm);
+            }
+            if (lane <= e)
+                lam[lane] = lm;
+            const uint8_t ai = lane < e ? aa[lane] : 0;
+            int lw = 0;  // log w_i, w_i = prod_{l != i} (a_i + a_l)
+            for (int l = 0; l < e; ++l)
+                if (l != lane)
+                    lw += glog[ai ^ aa[l]];
+            lw %= 255;
+            if (lane < e)
+                lws[lane] = (uint8_t)lw;
+            lds_sync();
+            if (lane < e) {  // row i of V_E^-1 by synthetic division: the parity sources q = nl + m
+                uint8_t qm = lam[e];
+                for (int m = e - 1; m >= 0; --m) {
+                    coef[lane * k + nl + m] = qm ? gexp[(glog[qm] + 255 - lw) % 255] : (uint8_t)0;
+                    if (m)
+                        qm = lam[m] ^ gmul(ai, qm);
+                }
+            }
+            if (lane < nl) {  // survivor q: Lambda(b_q) / ((b_q + a_i) w_i)
+                const uint8_t bq = gexp[lv[lane]];
+                int lb = 0;
+                for (int l = 0; l < e; ++l)
+                    lb += glog[bq ^ aa[l]];
+                lb %= 255;
+                for (int i = 0; i < e; ++i)
+                    coef[i * k + lane] = gexp[(lb + 2 * 255 - glog[bq ^ aa[i]] - lws[i]) % 255];
+            }
+        }
+    }
+    __syncthreads();
+    if (bad) {
+        if (blockIdx.x == 0 && threadIdx.x == 0)
+            a.status[b] = -2;
+        return;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0)
+        a.status[b] = 0;
+    const int j0 = wave * k / SPL, j1 = (wave + 1) * k / SPL;
+    const long long off = (long long)blockIdx.x * 2048 + lane * 32;
+    const uint32_t loff = off + 32 <= a.len ? (uint32_t)off : 0u;
+    const uint32_t m4 = vconst(0x0F0F0F0Fu), m2 = vconst(0x33333333u), m1 = vconst(0x55555555u);
+    uint4* mine = lds[wave];
+    const uint32_t base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint4*)mine;
+    asm volatile(RSGPU_TC_ZERO ::: RSGPU_TC_ACC_CLOBBERS);
+    for (int g0 = j0; g0 < j1; g0 += 4) {
+        const int nt = min(4, j1 - g0);
+        for (int t = 0; t < nt; ++t) {
+            const int q = g0 + t;
+            const uint8_t* row = q < nl ? a.src + ((size_t)b * k + lv[q]) * a.pitch
+                                        : a.par + ((size_t)b * e + (q - nl)) * a.pitch;
+            glds32(row, loff, base + (uint32_t)(t * 2 * 64 * 16));
+        }
+        // lane 16 t + w: dword w of source g0 + t's 8 handler addresses
+        uint32_t av = 0;
+        {
+            const int t = lane >> 4, s = (lane & 15) >> 1;
+            if (t < nt) {
+                const int c = s < e ? coef[s * k + g0 + t] : 0;
+                const unsigned long long ad =
+                    a.map_base + (unsigned long long)(a.map_copy[s] * 256 + c) * (unsigned long long)a.map_stride;
+                av = (lane & 1) ? (uint32_t)(ad >> 32) : (uint32_t)ad;
+            }
+        }
+        wait_vm(0);
+        for (int t = 0; t < nt; ++t) {
+            uint4 u = mine[(t * 2 + 0) * 64 + lane];
+            uint4 v = mine[(t * 2 + 1) * 64 + lane];
+            uint32_t W[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
+            tr8(W, m4, m2, m1);
+            mine[(t * 2 + 0) * 64 + lane] = make_uint4(W[0], W[1], W[2], W[3]);
+            mine[(t * 2 + 1) * 64 + lane] = make_uint4(W[4], W[5], W[6], W[7]);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        const uint32_t la = base + lane * 16;
+#define RSGPU_TC_RUNV(N)                                                                          \
+    asm volatile(RSGPU_TC_CHUNKV##N                                                               \
+                 :                                                                                \
+                 : [la] "v"(la), [av] "v"(av)                                                     \
+                 : RSGPU_TC_CLOBBERS, RSGPU_TC_ACC_CLOBBERS, "memory")
+        switch (nt) {
+        case 1: RSGPU_TC_RUNV(1); break;
+        case 2: RSGPU_TC_RUNV(2); break;
+        case 3: RSGPU_TC_RUNV(3); break;
+        default: RSGPU_TC_RUNV(4); break;
+        }
+#undef RSGPU_TC_RUNV
+        // the next group reuses this wave's part and av
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+    uint32_t* part = reinterpret_cast<uint32_t*>(mine);
+    [&]<int... Ss>(std::integer_sequence<int, Ss...>) {
+        (
+            [&] {
+                if (Ss < e) {
+                    uint32_t W[8];
+                    read_slot<Ss>(W);
+#pragma unroll
+                    for (int q = 0; q < 8; ++q)
+                        part[(Ss * 8 + q) * 64 + lane] = W[q];
+                }
+            }(),
+            ...);
+    }(std::make_integer_sequence<int, 8>{});
+    __syncthreads();
+    if (off + 32 > a.len)
+        return;
+    for (int r = wave; r < e; r += SPL) {
+        uint32_t W[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+        for (int w = 0; w < SPL; ++w) {
+            const uint32_t* pw = reinterpret_cast<const uint32_t*>(lds[w]);
+#pragma unroll
+            for (int q = 0; q < 8; ++q)
+                W[q] ^= pw[(r * 8 + q) * 64 + lane];
+        }
+        tr8(W, m4, m2, m1);
+        store32(a.out + ((size_t)b * e + r) * a.pitch, off, W);
+    }
+}
+
 }  // namespace tc
 
 hipError_t tc_query_handlers(unsigned long long* d_out, hipStream_t st)
@@ -267,6 +539,25 @@ int tc_slot_copy(int slot)
 {
     static constexpr int copy[8] = RSGPU_TC_SLOT_COPY;
     return copy[slot & 7];
+}
+
+hipError_t launch_rs_tc_split(const TcArgs& a, long long blocks, hipStream_t st)
+{
+    if (a.rows <= 0 || a.rows > 8 || a.k < 4)
+        return hipErrorInvalidValue;
+    dim3 grid((unsigned)((a.len + 2047) / 2048), (unsigned)blocks);
+    hipLaunchKernelGGL(tc::k_rs_tc_split<4>, grid, dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_rs_tc_fused(const TcFusedArgs& a, hipStream_t st)
+{
+    if (a.e <= 0 || a.e > 8 || a.k <= 0 || a.k > 64 || a.k < a.e || a.len % 32 || a.blocks <= 0 ||
+        a.blocks > 65535)
+        return hipErrorInvalidValue;
+    dim3 grid((unsigned)((a.len + 2047) / 2048), (unsigned)a.blocks);
+    hipLaunchKernelGGL(tc::k_rs_tc_fused<4>, grid, dim3(256), 0, st, a);
+    return hipGetLastError();
 }
 
 hipError_t launch_rs_tc(const TcArgs& a, long long blocks, hipStream_t st)

@@ -179,6 +179,7 @@ int tc_init(rsgpu_ctx* ctx)
         return -1;
     }
     std::memcpy(ctx->h_tc_table, h, sizeof h);
+    ctx->tc_base = se[0];
     ctx->d_tc_table = d;
     ctx->tc_state = 1;
     return 1;
@@ -354,10 +355,31 @@ void tc_fill_addr(const rsgpu_ctx* ctx, const uint8_t* coef, int k, int rows, un
 // d_dsts [B][rows] device row-pointer tables, d_addr the pass-layout
 // handler addresses, addr_stride elements between blocks' tables (0: one
 // table shared by every block).
+// (block, 2 KB tile) pairs below which a threaded-code pass of <= 8 rows
+// splits each tile's sources over four waves (k_rs_tc_split): one wave per
+// tile leaves most of the 1024 SIMDs idle and walks every source in series
+// (C2: one block, 489 tiles)
+constexpr long long kTcSplitMaxWork = 2048;
+
 int tc_launch(rsgpu_ctx* ctx, const char* name, const uint8_t* const* d_srcs, uint8_t* const* d_dsts,
               const unsigned long long* d_addr, long long addr_stride, int k, int rows, long long len,
               long long blocks, const int* d_status)
 {
+    if (rows <= 8 && k >= 4 && (len + 2047) / 2048 * blocks < kTcSplitMaxWork) {
+        TcArgs t{};
+        t.srcs = d_srcs;
+        t.dsts = d_dsts;
+        t.dst_stride = rows;
+        t.addr = d_addr;
+        t.addr_stride = addr_stride;
+        t.k = k;
+        t.rows = rows;
+        t.len = len;
+        t.status = d_status;
+        KTimer kt(ctx, name, (size_t)blocks);
+        RS_HIP(ctx, launch_rs_tc_split(t, blocks, ctx->stream));
+        return RSGPU_OK;
+    }
     for (int p = 0; p < tc_passes(rows); ++p) {
         TcArgs t{};
         t.srcs = d_srcs;
@@ -847,6 +869,13 @@ int rsgpu_encode_blocks(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch, 
     // Fast paths: the gf_gen_rs_matrix code with compile-time coefficients,
     // bit-sliced (len % 32 == 0) or nibble-table (len % 4 == 0).
     const bool compiled_ok = ctx->encode_kernel == RSGPU_ENCODE_AUTO || ctx->encode_kernel == RSGPU_ENCODE_COMPILED;
+    if (compiled_ok && !coef && aligned && len % 32 == 0 && rs_bitsliced_split_available(k, e) &&
+        (long long)((len + 2047) / 2048 * blocks) < kTcSplitMaxWork) {
+        KTimer kt(ctx, "k_rs_bs_split(encode)", blocks);
+        RS_HIP(ctx, launch_rs_bitsliced_split(k, e, d_src, d_parity, (long long)pitch, (long long)len,
+                                              (long long)blocks, ctx->stream));
+        return RSGPU_OK;
+    }
     if (compiled_ok && !coef && aligned && len % 32 == 0 && rs_bitsliced_available(k, e)) {
         KTimer kt(ctx, "k_rs_bs(encode)", blocks);
         RS_HIP(ctx, launch_rs_bitsliced(k, e, d_src, d_parity, (long long)pitch, (long long)len,
@@ -1270,6 +1299,36 @@ int rsgpu_decode_blocks(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch, 
             if (rc)
                 return rc;
         }
+        return RSGPU_OK;
+    }
+    // A small batch of the one-matrix decode with few rows (C2: one block of
+    // (16, 4, 1e6)): the decode rows are built inside the decode kernel, one
+    // launch instead of prepare + apply (k_rs_tc_fused)
+    if (e > 0 && e <= 8 && k <= 64 && len > 0 && blocks > 0 &&
+        decode_plan(ctx, k, e, len, pitch, blocks, d_src, d_parity, d_out) == Plan::one_matrix &&
+        (long long)((len + 2047) / 2048 * blocks) < kTcSplitMaxWork) {
+        int rc = check_geom(ctx, k, e, len, pitch, blocks);
+        if (rc)
+            return rc;
+        if (!d_err || !d_status)
+            return fail(ctx, RSGPU_ERR_ARG, "rsgpu_decode_blocks: bad arguments");
+        TcFusedArgs f{};
+        f.k = k;
+        f.e = e;
+        f.len = (long long)len;
+        f.pitch = (long long)pitch;
+        f.blocks = (long long)blocks;
+        f.err = d_err;
+        f.src = d_src;
+        f.par = d_parity;
+        f.out = d_out;
+        f.status = d_status;
+        f.map_base = ctx->tc_base;
+        f.map_stride = tc_handler_stride();
+        for (int sl = 0; sl < 8; ++sl)
+            f.map_copy[sl] = tc_slot_copy(sl);
+        KTimer kt(ctx, "k_rs_tc_fused(decode)", blocks);
+        RS_HIP(ctx, launch_rs_tc_fused(f, ctx->stream));
         return RSGPU_OK;
     }
     int rc = rsgpu_decode_prepare(ctx, k, e, len, pitch, blocks, d_src, d_parity, d_err, d_out,

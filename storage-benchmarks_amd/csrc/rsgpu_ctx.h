@@ -22,6 +22,7 @@ struct rsgpu_ctx {
     // -1 = unavailable (k_dot_generic serves instead)
     unsigned long long* d_tc_table = nullptr;
     unsigned long long h_tc_table[2048] = {};
+    unsigned long long tc_base = 0;  // first handler (the table is tc_base + i * stride)
     int tc_state = 0;
     int decode_kernel = RSGPU_DECODE_AUTO;
     // executable device memory for the generated decode code (rs_jit.h):

@@ -280,3 +280,83 @@ def test_encode_t0_pairing_chunk():
                     exp |= ge.mat_row(ge.gf_pow2(r * T), b) << (8 * T)
                 assert acc[o] == exp, (K, E, C, R0, o)
     assert npair > 0
+
+
+RDL = re.compile(r"v_readlane_b32 s(\d+), %\[av\], (\d+)")
+
+
+@pytest.mark.parametrize("nt", range(1, 5))
+def test_chunk_v_dispatch(nt):
+    """gen_tc_handlers.chunk_v (the fused small-batch decode's chunk): the
+    handler addresses come from lanes 16 t + i of one VGPR by v_readlane
+    instead of a scalar load, into the bank the scalar load would fill; the
+    chunk must accumulate the same products as chunk() (test_chunk_dispatch),
+    and every address word must be read before its first use."""
+    rng = random.Random(300 + nt)
+    src = [[rng.randrange(256) for _ in range(32)] for _ in range(nt)]
+    coef = [[rng.randrange(256) for _ in range(8)] for _ in range(nt)]
+    acc0 = [[rng.randrange(256) for _ in range(32)] for _ in range(8)]
+    regs = {i: 0 for i in range(256)}
+    for s in range(8):
+        for a, v in enumerate(planes(acc0[s])):
+            regs[g.ACC + 8 * s + a] = v
+    sregs, idx, banks = {}, None, (g.BANK[0], g.BANK[1])
+    code = g.chunk_v(nt)
+    assert not any(i.startswith("s_load") for i in code)
+    for i in code:
+        m = DS.match(i)
+        if m:
+            lo, hi, off = int(m.group(1)), int(m.group(2)), int(m.group(3))
+            t, half = off // g.LDS_T, (off % g.LDS_T) // g.LDS_H
+            p = planes(src[t])
+            for q in range(hi - lo + 1):
+                regs[lo + q] = p[4 * half + q]
+            continue
+        m = RDL.match(i)
+        if m:
+            sreg, lane = int(m.group(1)), int(m.group(2))
+            t, word = lane // 16, lane % 16
+            bank = banks[0] if sreg < banks[1] else banks[1]
+            assert sreg - bank == word and t < nt
+            if word % 2 == 0:  # low half of (slot word/2)'s address
+                sregs[sreg] = (word // 2, coef[t][word // 2])
+            continue
+        if i.startswith("s_set_gpr_idx_on"):
+            idx = int(i.split()[1].rstrip(","))
+        elif i.startswith("s_set_gpr_idx_idx"):
+            idx = int(i.split()[1])
+        elif i.startswith("s_set_gpr_idx_off"):
+            idx = None
+        elif i.startswith("s_mov_b64"):
+            m = SMOV.match(i)
+            sregs[int(m.group(1))] = sregs[int(m.group(2))]
+        elif i.startswith("s_swappc"):
+            rel = idx or 0
+            slot, c = sregs[int(SWAP.match(i).group(1))]
+            copy = g.SLOT_COPY[slot]
+            while True:
+                body = g.handler(c, copy)
+                for h in body:
+                    if h.startswith("s_"):
+                        continue
+                    mm = INSN.match(h)
+                    d = int(mm.group(2)) + rel
+                    ops = [int(x) for x in mm.groups()[2:] if x]
+                    ops[0] += rel
+                    val = 0
+                    for o in ops:
+                        val ^= regs[o]
+                    regs[d] = val
+                tgt = int(SETPC.search(" ".join(body)).group(1))
+                if tgt == g.RET:
+                    break
+                slot, c = sregs[tgt]
+                copy += 1
+        elif not i.startswith("s_"):
+            assert idx is None, i
+            run([i], regs)
+    for s in range(8):
+        exp = list(acc0[s])
+        for t in range(nt):
+            exp = [x ^ g.gf_mul(coef[t][s], y) for x, y in zip(exp, src[t])]
+        assert unplanes([regs[g.ACC + 8 * s + a] for a in range(8)]) == exp, (nt, s)

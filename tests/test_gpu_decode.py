@@ -434,12 +434,13 @@ def test_batch_beyond_grid_limit(ctx, orc, kernel):
         ctx.set_decode_kernel("auto")
 
 
-@pytest.mark.parametrize("blocks,name", [(1, "k_rs_tc(decode)"), (9, "k_rs_jit(decode)")])
+@pytest.mark.parametrize("blocks,name", [(1, "k_rs_tc_fused(decode)"), (9, "k_rs_jit(decode)")])
 def test_auto_decode_kernel_by_batch_work(ctx, blocks, name):
-    """AUTO decodes a batch with fewer than 4096 (block, 2 KB tile) pairs
-    through threaded code (the generated code's emission launch is not paid
-    back: C2, one full-row block) and larger batches through generated code;
-    both with the erased rows poisoned, recovered bytes intact."""
+    """AUTO decodes a batch with fewer than 2048 (block, 2 KB tile) pairs and
+    e <= 8 in ONE launch (k_rs_tc_fused: decode rows built in the kernel,
+    threaded code; C2, one full-row block) and larger batches through
+    generated code; both with the erased rows poisoned, recovered bytes
+    intact."""
     k, e, L = 16, 4, 1000000
     ctx.set_decode_kernel("auto")
     enc = rsgpu.GpuEncoder(k, L, e, blocks=blocks, seed=29, ctx=ctx)
@@ -598,3 +599,35 @@ def test_host_resident_api_poisoned(ctx, orc, k, e, L, B):
     data = [keep[0, j].numpy() for j in range(k)]
     rc, rec = orc.decode_block(data, [h_par[0, i].numpy() for i in range(e)], dec.err_host[0])
     assert rc == 0 and all((h_out[0, i].numpy() == rec[i]).all() for i in range(e))
+
+
+@pytest.mark.parametrize("k,e,L,B", [(16, 4, 1000000, 1), (16, 8, 64000, 3), (64, 8, 100000, 2), (3, 1, 4096, 4),
+                                     (5, 4, 2080, 7), (40, 7, 6144, 5), (9, 9, 2048, 1)])
+def test_fused_small_decode(ctx, orc, k, e, L, B):
+    """The one-launch small-batch decode (k_rs_tc_fused): decode rows in
+    closed form inside the kernel, sources split over four waves, partial
+    rows reduced in LDS; erased rows poisoned; ragged tiles (L % 2048), k
+    below the wave count, e == k; block 0 also against the oracle, and a
+    malformed list in the last block fails that block only (status -2)."""
+    ctx.set_decode_kernel("auto")
+    enc = rsgpu.GpuEncoder(k, L, e, blocks=B, seed=61, ctx=ctx)
+    enc.encode_all()
+    dec = rsgpu.GpuDecoder(k, L, e, blocks=B, seed=61, ctx=ctx)
+    ctx.timing_read()
+    ctx.timing_enable(True)
+    ok = decode_poisoned(ctx, enc, dec)
+    names = [n for n, _, _ in ctx.timing_read()]
+    ctx.timing_enable(False)
+    assert ok and names == ["k_rs_tc_fused(decode)"], names
+    data = [enc.src.view(B, k, enc.pitch)[0, j, :L].cpu().numpy() for j in range(k)]
+    rc, rec = orc.decode_block(data, list(enc.parity_rows(0)), dec.err_host[0])
+    got = dec.recovered_rows(0)
+    assert rc == 0 and all((got[i] == rec[i]).all() for i in range(e))
+    if B > 1 and e > 1:
+        bad = dec.err_host.copy()
+        bad[B - 1, :2] = bad[B - 1, 1::-1]  # not ascending
+        dec.err.copy_(torch.from_numpy(bad).view(dec.err.shape))
+        dec.decode_all(enc)
+        torch.cuda.synchronize()
+        st = dec.status.cpu().numpy()
+        assert st[B - 1] == -2 and (st[:B - 1] == 0).all(), st
