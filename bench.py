@@ -428,9 +428,9 @@ def valu_roofline(counters, kernel, ceiling):
 
 
 def valu_ceiling(path):
-    """Measured issue ceiling (SIMD cycles per VALU) at 4 waves per SIMD, or None."""
+    """Best measured issue rate (SIMD cycles per VALU, any occupancy), or None."""
     try:
-        return json.load(open(path))["waves_per_simd_4"]["simd_cycles_per_valu"]
+        return json.load(open(path))["best"]["simd_cycles_per_valu"]
     except (OSError, KeyError, ValueError):
         return None
 

@@ -363,12 +363,47 @@ template <int SPL>
 __global__ __launch_bounds__(64 * SPL) __attribute__((amdgpu_num_vgpr(64))) void k_rs_tc_fused(TcFusedArgs a)
 {
     __shared__ uint4 lds[SPL][C * 2 * 64];  // per wave: its sources, then its partial rows
-    __shared__ uint8_t gexp[512], glog[256], coef[8 * 64], lv[64];
+    __shared__ uint8_t gexp[512], glog[256], coef[8 * 64], lvw[SPL][64];
     __shared__ uint8_t aa[8], lam[16], lws[8];
-    __shared__ int bad;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     const int b = blockIdx.y, k = a.k, e = a.e, nl = k - e;
+    // every wave: its block's erasure list, validated, and the survivors
+    // (ascending) -- all it needs to start its own source loads at once,
+    // before the decode rows exist
+    const int j = lane < e ? a.err[(size_t)b * e + lane] : 255;  // lane i: erased original j_i
+    const int jp = __shfl_up(j, 1);
+    if (__ballot(lane < e && (j >= k || (lane > 0 && j <= jp))) != 0) {  // strictly ascending, < k
+        if (blockIdx.x == 0 && threadIdx.x == 0)
+            a.status[b] = -2;
+        return;  // uniform per workgroup
+    }
+    bool er = false;
+    for (int i = 0; i < e; ++i)
+        er |= __builtin_amdgcn_readlane(j, i) == lane;
+    const unsigned long long surv = __ballot(lane < k && !er);
+    const unsigned rank = __builtin_amdgcn_mbcnt_hi((unsigned)(surv >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)surv, 0u));
+    uint8_t* lv = lvw[wave];
+    if (lane < k && !er)
+        lv[rank] = (uint8_t)lane;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const int j0 = wave * k / SPL, j1 = (wave + 1) * k / SPL;
+    const long long off = (long long)blockIdx.x * 2048 + lane * 32;
+    const uint32_t loff = off + 32 <= a.len ? (uint32_t)off : 0u;
+    uint4* mine = lds[wave];
+    const uint32_t base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint4*)mine;
+    auto issue = [&](int g0) {
+        for (int t = 0; t < min(4, j1 - g0); ++t) {
+            const int q = g0 + t;
+            const uint8_t* row = q < nl ? a.src + ((size_t)b * k + lv[q]) * a.pitch
+                                        : a.par + ((size_t)b * e + (q - nl)) * a.pitch;
+            glds32(row, loff, base + (uint32_t)(t * 2 * 64 * 16));
+        }
+    };
+    if (j0 < j1)
+        issue(j0);
+    // the decode rows (closed form, as k_decode_prepare_syn) by wave 0 while
+    // the loads are in flight
     for (int i = threadIdx.x; i < 512; i += 64 * SPL) {
         gexp[i] = kGfTc.exp[i];
         if (i < 256)
@@ -378,83 +413,52 @@ __global__ __launch_bounds__(64 * SPL) __attribute__((amdgpu_num_vgpr(64))) void
     if (wave == 0) {  // the whole wave runs every statement; lanes select what they write
         auto gmul = [&](uint8_t x, uint8_t y) -> uint8_t { return (x && y) ? gexp[glog[x] + glog[y]] : (uint8_t)0; };
         auto lds_sync = [] { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); };
-        const int j = lane < e ? a.err[(size_t)b * e + lane] : 255;  // lane i: erased original j_i
-        const int jp = __shfl_up(j, 1);
-        const bool badl = lane < e && (j >= k || (lane > 0 && j <= jp));  // strictly ascending, < k
-        const bool anybad = __ballot(badl) != 0;
-        if (lane == 0)
-            bad = anybad;
-        if (!anybad) {  // wave-uniform
-            if (lane < e)
-                aa[lane] = gexp[j];  // a_i = 2^(j_i)
-            lds_sync();
-            int below = 0;  // survivors, ascending
-            bool er = false;
-            for (int i = 0; i < e; ++i) {
-                const int ji = glog[aa[i]];
-                below += ji < lane;
-                er |= ji == lane;
+        if (lane < e)
+            aa[lane] = gexp[j];  // a_i = 2^(j_i)
+        lds_sync();
+        uint8_t lm = lane == 0 ? 1 : 0;  // Lambda(z) = prod (z + a_l): lane m, coefficient of z^m
+        for (int l = 0; l < e; ++l) {
+            const int prev = __shfl_up((int)lm, 1);
+            lm = (uint8_t)(lane == 0 ? 0 : prev) ^ gmul(aa[l], lm);
+        }
+        if (lane <= e)
+            lam[lane] = lm;
+        const uint8_t ai = lane < e ? aa[lane] : 0;
+        int lw = 0;  // log w_i, w_i = prod_{l != i} (a_i + a_l)
+        for (int l = 0; l < e; ++l)
+            if (l != lane)
+                lw += glog[ai ^ aa[l]];
+        lw %= 255;
+        if (lane < e)
+            lws[lane] = (uint8_t)lw;
+        lds_sync();
+        if (lane < e) {  // row i of V_E^-1 by synthetic division: the parity sources q = nl + m
+            uint8_t qm = lam[e];
+            for (int m = e - 1; m >= 0; --m) {
+                coef[lane * k + nl + m] = qm ? gexp[(glog[qm] + 255 - lw) % 255] : (uint8_t)0;
+                if (m)
+                    qm = lam[m] ^ gmul(ai, qm);
             }
-            if (lane < k && !er)
-                lv[lane - below] = (uint8_t)lane;
-            uint8_t lm = lane == 0 ? 1 : 0;  // Lambda(z) = prod (z + a_l): lane m, coefficient of z^m
-            for (int l = 0; l < e; ++l) {
-                const int prev = __shfl_up((int)lm, 1);
-                lm = (uint8_t)(lane == 0 ? 0 : prev) ^ gmul(aa[l], lm);
-            }
-            if (lane <= e)
-                lam[lane] = lm;
-            const uint8_t ai = lane < e ? aa[lane] : 0;
-            int lw = 0;  // log w_i, w_i = prod_{l != i} (a_i + a_l)
+        }
+        if (lane < nl) {  // survivor q: Lambda(b_q) / ((b_q + a_i) w_i)
+            const uint8_t bq = gexp[lv[lane]];
+            int lb = 0;
             for (int l = 0; l < e; ++l)
-                if (l != lane)
-                    lw += glog[ai ^ aa[l]];
-            lw %= 255;
-            if (lane < e)
-                lws[lane] = (uint8_t)lw;
-            lds_sync();
-            if (lane < e) {  // row i of V_E^-1 by synthetic division: the parity sources q = nl + m
-                uint8_t qm = lam[e];
-                for (int m = e - 1; m >= 0; --m) {
-                    coef[lane * k + nl + m] = qm ? gexp[(glog[qm] + 255 - lw) % 255] : (uint8_t)0;
-                    if (m)
-                        qm = lam[m] ^ gmul(ai, qm);
-                }
-            }
-            if (lane < nl) {  // survivor q: Lambda(b_q) / ((b_q + a_i) w_i)
-                const uint8_t bq = gexp[lv[lane]];
-                int lb = 0;
-                for (int l = 0; l < e; ++l)
-                    lb += glog[bq ^ aa[l]];
-                lb %= 255;
-                for (int i = 0; i < e; ++i)
-                    coef[i * k + lane] = gexp[(lb + 2 * 255 - glog[bq ^ aa[i]] - lws[i]) % 255];
-            }
+                lb += glog[bq ^ aa[l]];
+            lb %= 255;
+            for (int i = 0; i < e; ++i)
+                coef[i * k + lane] = gexp[(lb + 2 * 255 - glog[bq ^ aa[i]] - lws[i]) % 255];
         }
     }
     __syncthreads();
-    if (bad) {
-        if (blockIdx.x == 0 && threadIdx.x == 0)
-            a.status[b] = -2;
-        return;
-    }
     if (blockIdx.x == 0 && threadIdx.x == 0)
         a.status[b] = 0;
-    const int j0 = wave * k / SPL, j1 = (wave + 1) * k / SPL;
-    const long long off = (long long)blockIdx.x * 2048 + lane * 32;
-    const uint32_t loff = off + 32 <= a.len ? (uint32_t)off : 0u;
     const uint32_t m4 = vconst(0x0F0F0F0Fu), m2 = vconst(0x33333333u), m1 = vconst(0x55555555u);
-    uint4* mine = lds[wave];
-    const uint32_t base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint4*)mine;
     asm volatile(RSGPU_TC_ZERO ::: RSGPU_TC_ACC_CLOBBERS);
     for (int g0 = j0; g0 < j1; g0 += 4) {
         const int nt = min(4, j1 - g0);
-        for (int t = 0; t < nt; ++t) {
-            const int q = g0 + t;
-            const uint8_t* row = q < nl ? a.src + ((size_t)b * k + lv[q]) * a.pitch
-                                        : a.par + ((size_t)b * e + (q - nl)) * a.pitch;
-            glds32(row, loff, base + (uint32_t)(t * 2 * 64 * 16));
-        }
+        if (g0 != j0)
+            issue(g0);  // the part is free: the previous group's dispatch is done
         // lane 16 t + w: dword w of source g0 + t's 8 handler addresses
         uint32_t av = 0;
         {

@@ -602,7 +602,7 @@ def test_host_resident_api_poisoned(ctx, orc, k, e, L, B):
 
 
 @pytest.mark.parametrize("k,e,L,B", [(16, 4, 1000000, 1), (16, 8, 64000, 3), (64, 8, 100000, 2), (3, 1, 4096, 4),
-                                     (5, 4, 2080, 7), (40, 7, 6144, 5), (9, 9, 2048, 1)])
+                                     (5, 4, 2080, 7), (40, 7, 6144, 5), (8, 8, 2048, 1)])
 def test_fused_small_decode(ctx, orc, k, e, L, B):
     """The one-launch small-batch decode (k_rs_tc_fused): decode rows in
     closed form inside the kernel, sources split over four waves, partial
