@@ -72,6 +72,7 @@ def parse(argv=None):
                    choices=["auto", "generated", "one_matrix", "general"])
     p.add_argument("--encode-kernel", default="auto",
                    choices=["auto", "compiled", "generated", "threaded"])
+    p.add_argument("--jitw-tiles", type=int, default=0, help=argparse.SUPPRESS)  # A/B hook
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-threads", type=int, default=None)
     p.add_argument("--no-ref-base", action="store_true",
@@ -600,6 +601,11 @@ def main(argv=None):
     ctx.set_torch_stream()
     ctx.set_decode_kernel(args.decode_kernel)
     ctx.set_encode_kernel(args.encode_kernel)
+    if args.jitw_tiles:
+        import ctypes
+        f = rsgpu.lib().rsgpu_internal_set_jitw_tiles
+        f.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        assert f(ctx._h, args.jitw_tiles) == 0
     alg = alg_bytes(k, e, L)
     rank_info = None
 

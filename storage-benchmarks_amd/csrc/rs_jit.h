@@ -225,16 +225,21 @@ struct Wide {
         return CL + 11 * hi + (n - below - 1);
     }
 
+    // the multiply-accumulate word of output plane b of slot s, for row b
+    // (mask m = mat_row(c, b)) of the coefficient's matrix
+    RJ_HD static uint64_t mac_word(uint8_t m, int s, int b)
+    {
+        const int acc = ACC + 8 * s + b, lo = m & 15, hi = m >> 4;
+        return lo && hi ? enc_bitop3_96(acc, acc, treg(0, lo), treg(1, hi))
+               : lo     ? enc_xor_e64(acc, acc, treg(0, lo))
+               : hi     ? enc_xor_e64(acc, acc, treg(1, hi))
+                        : (uint64_t)S_NOP0 << 32 | S_NOP0;
+    }
+
     RJ_HD static void mac_words(uint8_t c, int s, uint64_t (&wd)[8])
     {
-        for (int b = 0; b < 8; ++b) {
-            const uint8_t m = mat_row(c, b);
-            const int acc = ACC + 8 * s + b, lo = m & 15, hi = m >> 4;
-            wd[b] = lo && hi ? enc_bitop3_96(acc, acc, treg(0, lo), treg(1, hi))
-                    : lo     ? enc_xor_e64(acc, acc, treg(0, lo))
-                    : hi     ? enc_xor_e64(acc, acc, treg(1, hi))
-                             : (uint64_t)S_NOP0 << 32 | S_NOP0;
-        }
+        for (int b = 0; b < 8; ++b)
+            wd[b] = mac_word(mat_row(c, b), s, b);
     }
 
     // 32-bit word i (< PRE / 4 = 28) of source t's preamble

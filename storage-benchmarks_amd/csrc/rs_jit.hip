@@ -254,12 +254,17 @@ __device__ __forceinline__ void read_slotw(uint32_t (&W)[8])
 // not allocate them itself, and the kernel descriptor still gives the wave
 // 168 VGPRs (.amdhsa_next_free_vgpr 168, no AGPRs), which only the asm and
 // the generated code touch.
-template <class W>
-__global__ __launch_bounds__(128) __attribute__((amdgpu_num_vgpr(40))) void k_rs_jitw(JitArgs a)
+// TPW > 1: one workgroup covers TPW consecutive column tiles of a block (2
+// TPW waves; wave w: tile w / 2, rows of wave w % 2), so the TPW waves with
+// the same rows run the same code between the same chunk barriers and share
+// its instruction-cache lines.
+template <class W, int TPW>
+__global__ __launch_bounds__(128 * TPW) __attribute__((amdgpu_num_vgpr(40))) void k_rs_jitw(JitArgs a)
 {
     constexpr int CS = W::CS, R = W::R;
-    __shared__ uint4 lds[2][CS * 2 * 64];
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    __shared__ uint4 lds[2][TPW][CS * 2 * 64];
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wave = wv & 1, tw = wv >> 1;  // rows of the wave, its tile in the workgroup
     const int lane = threadIdx.x & 63;
     int b = blockIdx.y;
     long long tile = blockIdx.x;
@@ -270,6 +275,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_num_vgpr(40))) void k_rs
         b = (int)(lin / gridDim.x);
         tile = lin - (unsigned)b * gridDim.x;
     }
+    tile = tile * TPW + tw;
     if (a.status && a.status[b] != 0)
         return;
     const int k = a.k;
@@ -277,14 +283,15 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_num_vgpr(40))) void k_rs
     const uint8_t* const* srcs = a.srcs + (size_t)b * k;
     uint8_t* const* dsts = a.dsts + (size_t)b * a.dst_stride;
     const uint8_t* code = a.code + (size_t)b * a.block_stride + (size_t)wave * nch * a.chunk_stride;
-    const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint4*)&lds[0][0];
+    const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint4*)&lds[0][tw][0];
+    constexpr uint32_t kBuf = TPW * CS * 2 * 64 * 16;  // bytes between the two chunk buffers
     const long long off = tile * 2048 + lane * 32;
-    const uint32_t loff = off + 32 <= a.len ? (uint32_t)off : 0u;
-    if (wave == 0)
+    const uint32_t loff = off + 32 <= a.len ? (uint32_t)off : 0u;  // tiles past the row re-read its head
+    if (wv == 0)
         asm volatile("s_icache_inv\n s_nop 15\n s_nop 15" ::: "memory");
     auto issue = [&](int ch) {
         const int c0 = ch * CS, nt = min(CS, k - c0);
-        const uint32_t base = lds0 + (uint32_t)((ch & 1) * CS * 2 * 64 * 16);
+        const uint32_t base = lds0 + (uint32_t)((ch & 1) * kBuf);
         for (int t = wave; t < nt; t += 2)
             glds32(sload_ptr(srcs + c0 + t), loff, base + (uint32_t)(t * 2 * 64 * 16));
     };
@@ -297,7 +304,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_num_vgpr(40))) void k_rs
     issue(0);
     for (int ch = 0; ch < nch; ++ch) {
         const int nt = min(CS, k - ch * CS);
-        uint4* buf = lds[ch & 1];
+        uint4* buf = lds[ch & 1][tw];
         wait_vm(0);
         {
             const uint32_t m4 = vconst(0x0F0F0F0Fu), m2 = vconst(0x33333333u), m1 = vconst(0x55555555u);
@@ -312,7 +319,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_num_vgpr(40))) void k_rs
         barrier_lds();
         if (ch + 1 < nch)
             issue(ch + 1);
-        const uint32_t la = lds0 + (uint32_t)((ch & 1) * CS * 2 * 64 * 16) + lane * 16;
+        const uint32_t la = lds0 + (uint32_t)((ch & 1) * kBuf) + lane * 16;
         const uint8_t* fn = code + (size_t)ch * a.chunk_stride;
         if constexpr (R == 16)
             asm volatile("s_swappc_b64 s[82:83], %[fn]"
@@ -421,6 +428,7 @@ __global__ __launch_bounds__(256) void k_jitw_emit(int k, int e, const uint8_t* 
 {
     constexpr int R = W::R, CS = W::CS;
     __shared__ uint8_t cw[R * 256];
+    __shared__ uint8_t mrow[256 * 8];  // row b of the matrix of coefficient c at mrow[8 c + b]
     const int b = blockIdx.y, w = blockIdx.x;
     if (status[b] != 0)
         return;
@@ -431,19 +439,32 @@ __global__ __launch_bounds__(256) void k_jitw_emit(int k, int e, const uint8_t* 
     const int sb = W::src_bytes(nslot);
     for (int i = threadIdx.x; i < nslot * k; i += blockDim.x)
         cw[i] = coef[((size_t)b * e + R * w) * k + i];
+    {  // the 256 matrices once per workgroup: thread c, column a = c 2^a
+        const int c = threadIdx.x;
+        uint8_t x = (uint8_t)c, row[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        for (int a = 0; a < 8; ++a) {
+#pragma unroll
+            for (int bb = 0; bb < 8; ++bb)
+                row[bb] |= (uint8_t)(((x >> bb) & 1) << a);
+            x = (uint8_t)((x << 1) ^ ((x & 0x80) ? 0x1D : 0));
+        }
+#pragma unroll
+        for (int bb = 0; bb < 8; ++bb)
+            mrow[8 * c + bb] = row[bb];
+    }
     __syncthreads();
-    for (int i = threadIdx.x; i < R * k; i += blockDim.x) {  // (source, slot) runs
-        const int q = i / R, s = i - q * R;
+    // (source, slot) runs of 64 bytes, one 16-byte quarter per thread, so a
+    // wave's store covers 1 KB of consecutive code
+    for (int i = threadIdx.x; i < R * k * 4; i += blockDim.x) {
+        const int run = i >> 2, j = i & 3;
+        const int q = run / R, s = run - q * R;
         if (s >= nslot)
             continue;
         const int ch = q / CS, t = q - ch * CS;
-        uint64_t wd[8];
-        W::mac_words(cw[s * k + q], s, wd);
-        uint4* dst = reinterpret_cast<uint4*>(cbase + (size_t)ch * stride + (size_t)t * sb + W::PRE + 64 * s);
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-            dst[j] = make_uint4((uint32_t)wd[2 * j], (uint32_t)(wd[2 * j] >> 32), (uint32_t)wd[2 * j + 1],
-                                (uint32_t)(wd[2 * j + 1] >> 32));
+        const uint8_t* mr = mrow + 8 * cw[s * k + q];
+        const uint64_t w0 = W::mac_word(mr[2 * j], s, 2 * j), w1 = W::mac_word(mr[2 * j + 1], s, 2 * j + 1);
+        reinterpret_cast<uint4*>(cbase + (size_t)ch * stride + (size_t)t * sb + W::PRE + 64 * s)[j] =
+            make_uint4((uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1, (uint32_t)(w1 >> 32));
     }
     constexpr int PW = W::PRE / 8;
     for (int i = threadIdx.x; i < PW * k; i += blockDim.x) {  // preambles
@@ -496,13 +517,24 @@ hipError_t launch_rs_jitw(const JitArgs& a, long long blocks, hipStream_t st)
 {
     if (!jitw_rows(a.rows) || a.dst_stride < a.rows || a.k <= 0 || !a.code || a.chunk_stride <= 0)
         return hipErrorInvalidValue;
-    dim3 grid((unsigned)((a.len + 2047) / 2048), (unsigned)blocks);
-    if (jitw_rows(a.rows) == 16)
-        hipLaunchKernelGGL(jitk::k_rs_jitw<jit::J16>, grid, dim3(128), 0, st, a);
-    else if (jitw_rows(a.rows) == 12)
-        hipLaunchKernelGGL(jitk::k_rs_jitw<jit::J12>, grid, dim3(128), 0, st, a);
-    else
-        hipLaunchKernelGGL(jitk::k_rs_jitw<jit::J10>, grid, dim3(128), 0, st, a);
+    const int tpw = a.tiles_per_wg >= 3 ? 3 : a.tiles_per_wg == 2 ? 2 : 1;
+    const long long ntile = (a.len + 2047) / 2048;
+    dim3 grid((unsigned)((ntile + tpw - 1) / tpw), (unsigned)blocks);
+    dim3 blk(128 * tpw);
+#define RSGPU_JW_LAUNCH(WT)                                                                          \
+    switch (tpw) {                                                                                   \
+    case 3: hipLaunchKernelGGL((jitk::k_rs_jitw<WT, 3>), grid, blk, 0, st, a); break;               \
+    case 2: hipLaunchKernelGGL((jitk::k_rs_jitw<WT, 2>), grid, blk, 0, st, a); break;               \
+    default: hipLaunchKernelGGL((jitk::k_rs_jitw<WT, 1>), grid, blk, 0, st, a); break;              \
+    }
+    if (jitw_rows(a.rows) == 16) {
+        RSGPU_JW_LAUNCH(jit::J16)
+    } else if (jitw_rows(a.rows) == 12) {
+        RSGPU_JW_LAUNCH(jit::J12)
+    } else {
+        RSGPU_JW_LAUNCH(jit::J10)
+    }
+#undef RSGPU_JW_LAUNCH
     return hipGetLastError();
 }
 

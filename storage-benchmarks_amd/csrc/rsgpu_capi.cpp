@@ -944,9 +944,15 @@ enum class Plan {
 };
 
 // column tiles (2 KB) per block from which AUTO decodes through generated
-// code; below kJitXcdTiles the decode runs in XCD-contiguous order
+// code (the two-wave layouts, 16 < e <= 32, run two tiles per workgroup and
+// pay from 16 tiles: C4 14.07 + 0.86 emission vs 15.44 ms threaded per 16384
+// blocks, profiles/r03_ab/c4_gen_vs_tc/); below kJitXcdTiles the 8-row
+// decode runs in XCD-contiguous order
 constexpr size_t kJitMinTiles = 48;
+constexpr size_t kJitwMinTiles = 16;
 constexpr size_t kJitXcdTiles = 128;
+
+size_t jit_min_tiles(int e) { return jitw_rows(e) ? kJitwMinTiles : kJitMinTiles; }
 // (block, tile) pairs per call from which AUTO pays the emission launch
 // (~10 us whatever the batch) for the ~4 ns per pair the generated code saves
 // over threaded code: C2 (one block, 489 tiles) decodes 16 us threaded
@@ -979,7 +985,7 @@ Plan decode_plan(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch, size_t 
     // (e <= 63); the threaded-code kernel takes e <= 32
     const bool gen_ok = e <= 63 && jit_probe(ctx) == 1 && want != RSGPU_DECODE_ONE_MATRIX &&
                         want != RSGPU_DECODE_GENERAL &&
-                        (want == RSGPU_DECODE_GENERATED || (len + 2047) / 2048 >= kJitMinTiles);
+                        (want == RSGPU_DECODE_GENERATED || (len + 2047) / 2048 >= jit_min_tiles(e));
     if (e > 32 && gen_ok)
         return Plan::generated;
     if (want == RSGPU_DECODE_GENERAL || e > 32)
@@ -989,10 +995,10 @@ Plan decode_plan(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch, size_t 
     // AUTO: generated code only when a block has enough column tiles to
     // amortise its ~160 KB of code (every tile's workgroup fetches all of
     // it): C3 / C5 (489 tiles) 25.2 / 15.0 ms vs 27 / 17.7 threaded; L =
-    // 128000 (63 tiles) 3.79 vs 3.94 ms; C4 (16 tiles) 14.7 + 1.25 emission
-    // vs 15.0 per 16384 blocks (profiles/r02_ab)
+    // 128000 (63 tiles) 3.79 vs 3.94 ms (8-row layout, profiles/r02_ab); C4
+    // (16 tiles) with two tiles per workgroup, above
     if (want == RSGPU_DECODE_AUTO &&
-        ((len + 2047) / 2048 < kJitMinTiles || (len + 2047) / 2048 * blocks < kJitMinWork))
+        ((len + 2047) / 2048 < jit_min_tiles(e) || (len + 2047) / 2048 * blocks < kJitMinWork))
         return Plan::one_matrix;
     return Plan::generated;
 }
@@ -1087,6 +1093,11 @@ int jit_decode_launch(rsgpu_ctx* ctx, int k, int e, size_t len, size_t blocks, c
         // 16-row kernel (23.3 vs 24.2 ms, profiles/r02_ab/jit_rows16/xcd_*.log),
         // where the 8-row kernel measured 1 % slower
         j.xcd_order = 1;
+        // two column tiles per workgroup: the waves with the same rows share
+        // their code's instruction-cache lines (C4 13.7 vs 14.2 ms per 16384
+        // blocks, C3 23.2-23.3 vs 23.4-23.5, C5 12.7-12.8 vs 12.8-12.9;
+        // three tiles: 20-30 % slower; profiles/r03_ab/tpw/)
+        j.tiles_per_wg = ctx->jitw_tpw ? ctx->jitw_tpw : 2;
         KTimer kt(ctx,
                   jitw_rows(e) == 16   ? "k_rs_jit16(decode)"
                   : jitw_rows(e) == 12 ? "k_rs_jit12(decode)"
@@ -1438,6 +1449,16 @@ int rsgpu_fill_synthetic(rsgpu_ctx* ctx, unsigned char* d_rows, size_t rows, siz
 // shared by every block (jit_prog.h, the GENERATED encode), for the CPU
 // suite to disassemble and interpret.  Returns the bytes needed, or -1;
 // writes only when out_bytes is large enough; *chunk_stride gets the stride.
+// Test / A-B hook (not part of include/rsgpu.h): column tiles per workgroup
+// of the two-wave generated decode (1, 2, 3; 0 = the library's choice).
+int rsgpu_internal_set_jitw_tiles(rsgpu_ctx* ctx, int n)
+{
+    if (!ctx || n < 0 || n > 3)
+        return RSGPU_ERR_ARG;
+    ctx->jitw_tpw = n;
+    return RSGPU_OK;
+}
+
 long long rsgpu_internal_jit_matrix_code(int k, int e, const unsigned char* coef, unsigned char* out,
                                          size_t out_bytes, int* chunk_stride, int max_ops)
 {

@@ -25,6 +25,7 @@ struct rsgpu_ctx {
     unsigned long long tc_base = 0;  // first handler (the table is tc_base + i * stride)
     int tc_state = 0;
     int decode_kernel = RSGPU_DECODE_AUTO;
+    int jitw_tpw = 0;  // k_rs_jitw column tiles per workgroup (0: by geometry)
     // executable device memory for the generated decode code (rs_jit.h):
     // grow-only; jit_state 0 = not probed, 1 = pool found, -1 = unavailable
     void* d_jit = nullptr;

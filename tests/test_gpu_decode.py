@@ -631,3 +631,26 @@ def test_fused_small_decode(ctx, orc, k, e, L, B):
         torch.cuda.synchronize()
         st = dec.status.cpu().numpy()
         assert st[B - 1] == -2 and (st[:B - 1] == 0).all(), st
+
+
+@pytest.mark.parametrize("tpw", [2, 3])
+@pytest.mark.parametrize("k,e,L,B", [(64, 32, 1000000, 2), (64, 32, 32000, 9), (100, 20, 6144, 3),
+                                     (48, 24, 14336, 2)])
+def test_jitw_tiles_per_workgroup(ctx, tpw, k, e, L, B):
+    """k_rs_jitw with 2 or 3 column tiles per workgroup (the A/B hook
+    rsgpu_internal_set_jitw_tiles): the same recovered bytes with the erased
+    rows poisoned, including tile counts that do not divide by the group
+    (489, 16, 3, 7 tiles per block)."""
+    import ctypes
+    f = rsgpu.lib().rsgpu_internal_set_jitw_tiles
+    f.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    ctx.set_decode_kernel("generated")
+    assert f(ctx._h, tpw) == 0
+    try:
+        enc = rsgpu.GpuEncoder(k, L, e, blocks=B, seed=71, ctx=ctx)
+        enc.encode_all()
+        dec = rsgpu.GpuDecoder(k, L, e, blocks=B, seed=71, ctx=ctx)
+        assert decode_poisoned(ctx, enc, dec)
+    finally:
+        f(ctx._h, 0)
+        ctx.set_decode_kernel("auto")
