@@ -73,6 +73,9 @@ def parse(argv=None):
     p.add_argument("--encode-kernel", default="auto",
                    choices=["auto", "compiled", "generated", "threaded"])
     p.add_argument("--jitw-tiles", type=int, default=0, help=argparse.SUPPRESS)  # A/B hook
+    # diagnostic: c4 batches from the third on keep the sources of two batches
+    # before (verification still checks every batch against its buffer)
+    p.add_argument("--no-regen", action="store_true", help=argparse.SUPPRESS)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-threads", type=int, default=None)
     p.add_argument("--no-ref-base", action="store_true",
@@ -525,7 +528,8 @@ def run_streamed(args, rsgpu, ctx, dev, rank, world, k, e, L, total_blocks):
                 s_gen.wait_event(ev_t[i - 1][1])
             if i >= 2:
                 s_gen.wait_event(ev_done[i - 2])  # batch i-2 (same buffers) verified
-            gen_ctx.fill_synthetic(enc.src, nb * k, L, enc.pitch, args.seed, b0 * k)
+            if i < 2 or not args.no_regen:
+                gen_ctx.fill_synthetic(enc.src, nb * k, L, enc.pitch, args.seed, b0 * k)
             dec.err.view(-1)[:nb * e].copy_(h_err[i & 1][:nb].reshape(-1), non_blocking=True)
             ev_gen[i].record(s_gen)
 

@@ -453,3 +453,42 @@ def test_host_io_ragged_chunks(ctx):
     assert r["verified"] and r["blocks"] == 70
     s = bench.host_io_rate(rsgpu, ctx, 16, 8, 64000, 6, seed=3, reps=1)
     assert s["verified"] and s["poisoned"]
+
+
+@pytest.mark.parametrize("k,e,kernel", [(64, 32, "generated"), (64, 32, "auto"), (100, 20, "generated"),
+                                        (16, 4, "auto")])
+def test_full_row_every_byte_vs_oracle(ctx, orc, k, e, kernel):
+    """One block of a BASELINE geometry at its full 1 MB rows, EVERY byte of
+    the parity and of the recovered rows against the CPU oracle (the round
+    trips above compare the whole batch with the originals on the device and
+    a 4 KiB window with the oracle).  The decode runs with the erased rows
+    poisoned, through the generated code (two tiles per workgroup) or AUTO's
+    choice for the call (threaded code; the one-launch small decode at
+    (16, 4))."""
+    L, B, seed = 1000000, 2, 4242
+    ctx.set_decode_kernel(kernel)
+    try:
+        enc = rsgpu.GpuEncoder(k, L, e, blocks=B, seed=seed, ctx=ctx)
+        enc.encode_all()
+        dec = rsgpu.GpuDecoder(k, L, e, blocks=B, seed=seed, ctx=ctx)
+        torch.cuda.synchronize()
+        blk = 1
+        data = [np.ascontiguousarray(s) for s in enc.source_rows(blk)]
+        ref = orc.encode_block(data, e)
+        par = enc.parity_rows(blk)
+        for p in range(e):
+            assert (par[p] == ref[p]).all(), p
+        src = enc.src.view(B, k, enc.pitch)
+        for b in range(B):
+            for j in dec.err_host[b]:
+                src[b, int(j), :L] = 0xA5
+        dec.decode_all(enc)
+        torch.cuda.synchronize()
+        assert dec.is_complete()
+        rc, rec = orc.decode_block(data, [np.ascontiguousarray(x) for x in par], dec.err_host[blk])
+        assert rc == 0
+        got = dec.recovered_rows(blk)
+        for i, j in enumerate(dec.err_host[blk]):
+            assert (got[i] == rec[i]).all() and (got[i] == data[int(j)]).all(), (i, int(j))
+    finally:
+        ctx.set_decode_kernel("auto")
