@@ -476,7 +476,8 @@ def alg_bytes(k, e, L):
     """Algorithmic HBM bytes per BLOCK of each kernel:
     (k + e) L for an encode or a decode (read k rows, write e)."""
     blk_op = float((k + e) * L)
-    return {"k_rs_bs(encode)": blk_op, "k_rs_encode_lh": blk_op, "k_dot_generic": blk_op,
+    return {"k_rs_bs(encode)": blk_op, "k_rs_bs_split(encode)": blk_op, "k_rs_tc_fused(decode)": blk_op,
+            "k_rs_encode_lh": blk_op, "k_dot_generic": blk_op,
             "k_dot_generic(decode)": blk_op,
             "k_rs_tc(encode)": blk_op, "k_rs_tc(decode)": blk_op, "k_rs_jit(decode)": blk_op,
             "k_rs_jit16(decode)": blk_op, "k_rs_jit10(decode)": blk_op, "k_rs_jit12(decode)": blk_op, "k_rs_jit(encode)": blk_op,

@@ -349,28 +349,33 @@ __global__ __launch_bounds__(64 * SPL) __attribute__((amdgpu_num_vgpr(64))) void
 }
 
 // The whole decode of a small batch in ONE launch (rsgpu_decode_blocks, C2:
-// one block of (16, 4, 1e6), e <= 8, k <= 64): every workgroup first builds
-// its block's e x k decode rows V_E^-1 [V_kept | I] in closed form (as
-// k_decode_prepare_syn, rs_kernels.hip: Lambda, w_i, Lambda(b_q), synthetic
-// division) with wave 0 and LDS tables, then runs k_rs_tc_split's work with
+// one block of (16, 4, 1e6), e <= 8, k <= 64): every wave first builds the
+// coefficients of its own sources from the e x k decode rows V_E^-1 [V_kept | I]
+// in closed form (the rows of k_decode_prepare_syn, rs_kernels.hip, as
+// Lagrange bases: logs for the survivors, Q_i = prod_{l != i} (z + a_l) built
+// lane-parallel in registers for the parity sources) while its source loads
+// fly, with no barrier, then runs k_rs_tc_split's work with
 // the handler addresses computed from the rows (handler of slot s for
 // coefficient c at map.base + (map.copy[s] 256 + c) map.stride) and handed
 // to the threaded code in a VGPR (RSGPU_TC_CHUNKV, v_readlane) instead of a
 // table in memory.  Saves the prepare launch and its table round trip.
-__device__ const GfTables kGfTc = make_gf_tables();
+alignas(16) __device__ const GfTables kGfTc = make_gf_tables();
 
-template <int SPL>
+template <int SPL, class H = TcHooks>
 __global__ __launch_bounds__(64 * SPL) __attribute__((amdgpu_num_vgpr(64))) void k_rs_tc_fused(TcFusedArgs a)
 {
+    typename H::Timer tp;
     __shared__ uint4 lds[SPL][C * 2 * 64];  // per wave: its sources, then its partial rows
-    __shared__ uint8_t gexp[512], glog[256], coef[8 * 64], lvw[SPL][64];
-    __shared__ uint8_t aa[8], lam[16], lws[8];
+    __shared__ uint32_t gtw[SPL][192];         // per wave: its copy of exp[512] | log[256]
+    __shared__ uint8_t coef[8 * 64], lvw[SPL][64];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     const int b = blockIdx.y, k = a.k, e = a.e, nl = k - e;
-    // every wave: its block's erasure list, validated, and the survivors
-    // (ascending) -- all it needs to start its own source loads at once,
-    // before the decode rows exist
+    // every wave: the GF tables and its block's erasure list (one round trip),
+    // the list validated, and the survivors (ascending) -- all it needs to
+    // start its own source loads at once, before the decode rows exist
+    const uint32_t* tsrc = reinterpret_cast<const uint32_t*>(&kGfTc);
+    const uint32_t t0 = tsrc[lane], t1 = tsrc[64 + lane], t2 = tsrc[128 + lane];
     const int j = lane < e ? a.err[(size_t)b * e + lane] : 255;  // lane i: erased original j_i
     const int jp = __shfl_up(j, 1);
     if (__ballot(lane < e && (j >= k || (lane > 0 && j <= jp))) != 0) {  // strictly ascending, < k
@@ -378,6 +383,13 @@ __global__ __launch_bounds__(64 * SPL) __attribute__((amdgpu_num_vgpr(64))) void
             a.status[b] = -2;
         return;  // uniform per workgroup
     }
+    tp.mark(0);
+    uint32_t* gw = gtw[wave];
+    gw[lane] = t0;
+    gw[64 + lane] = t1;
+    gw[128 + lane] = t2;
+    const uint8_t* gexp = reinterpret_cast<const uint8_t*>(gw);
+    const uint8_t* glog = gexp + 512;
     bool er = false;
     for (int i = 0; i < e; ++i)
         er |= __builtin_amdgcn_readlane(j, i) == lane;
@@ -402,55 +414,75 @@ __global__ __launch_bounds__(64 * SPL) __attribute__((amdgpu_num_vgpr(64))) void
     };
     if (j0 < j1)
         issue(j0);
-    // the decode rows (closed form, as k_decode_prepare_syn) by wave 0 while
-    // the loads are in flight
-    for (int i = threadIdx.x; i < 512; i += 64 * SPL) {
-        gexp[i] = kGfTc.exp[i];
-        if (i < 256)
-            glog[i] = kGfTc.log[i];
+    tp.mark(1);
+    // While the loads fly, each wave builds the coefficients of its own
+    // sources (closed form, the rows k_decode_prepare_syn builds): row i of
+    // V_E^-1 [V_kept | I] is the Lagrange basis L_i(z) = Q_i(z) / w_i with
+    // Q_i = prod_{l != i} (z + a_l), a_l = 2^(j_l), w_i = Q_i(a_i); survivor q
+    // gets L_i(b_q) through logs, parity source nl + m the coefficient of z^m.
+    const int al = lane < e ? gexp[j] : 0;  // lane l: a_l
+    // a_l in SGPRs, unused l < 8 marked (readlane outside any ?:, which clang
+    // lowers to branches around a convergent call)
+    int A[8];
+    bool use[8];
+#pragma unroll
+    for (int l = 0; l < 8; ++l) {
+        A[l] = __builtin_amdgcn_readlane(al, l);
+        use[l] = l < e;
     }
-    __syncthreads();
-    if (wave == 0) {  // the whole wave runs every statement; lanes select what they write
-        auto gmul = [&](uint8_t x, uint8_t y) -> uint8_t { return (x && y) ? gexp[glog[x] + glog[y]] : (uint8_t)0; };
-        auto lds_sync = [] { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); };
-        if (lane < e)
-            aa[lane] = gexp[j];  // a_i = 2^(j_i)
-        lds_sync();
-        uint8_t lm = lane == 0 ? 1 : 0;  // Lambda(z) = prod (z + a_l): lane m, coefficient of z^m
+    auto pick = [&](int idx) {  // a_idx, idx per lane
+        int r = 0;
+#pragma unroll
+        for (int l = 0; l < 8; ++l)
+            r = idx == l ? A[l] : r;
+        return r;
+    };
+    auto log_w = [&](int i) {  // log w_i = sum_{l != i} log (a_i + a_l)
+        const int ai = pick(i);
+        int sw = 0;
+#pragma unroll
+        for (int l = 0; l < 8; ++l)
+            sw += glog[(use[l] && l != i) ? ai ^ A[l] : 1];  // log 1 = 0
+        return sw % 255;
+    };
+    const int s1 = min(j1, nl);
+    for (int p = j0 * 8; p < s1 * 8; p += 64) {  // (survivor q, row i) on lane 8 q + i
+        const int q = (p + lane) >> 3, i = lane & 7;
+        if (q < s1 && i < e) {
+            const int bq = gexp[lv[q]];
+            int lb = 0;  // log Lambda(b_q)
+#pragma unroll
+            for (int l = 0; l < 8; ++l)
+                lb += glog[use[l] ? bq ^ A[l] : 1];
+            coef[i * k + q] = gexp[(lb + 2 * 255 - glog[bq ^ pick(i)] - log_w(i)) % 255];
+        }
+    }
+    if (j1 > nl) {  // parity sources: Q_i's coefficients, z^m on lane 8 i + m
+        const int i = lane >> 3, m = lane & 7;
+        int J[8];
+#pragma unroll
+        for (int l = 0; l < 8; ++l)
+            J[l] = __builtin_amdgcn_readlane(j, l);
+        int ji = 0;
+#pragma unroll
+        for (int l = 0; l < 8; ++l)
+            ji = i == l ? J[l] : ji;
+        const int tv = gexp[ji + m];  // lane 8 l + c: a_l x^c = 2^(j_l + c)
+        int qv = m == 0;
         for (int l = 0; l < e; ++l) {
-            const int prev = __shfl_up((int)lm, 1);
-            lm = (uint8_t)(lane == 0 ? 0 : prev) ^ gmul(aa[l], lm);
+            int pr = 0;  // a_l q_m: the x^c multiples of a_l where q_m has bit c
+#pragma unroll
+            for (int c = 0; c < 8; ++c)
+                pr ^= __builtin_amdgcn_readlane(tv, l * 8 + c) & -((qv >> c) & 1);
+            int sh = __builtin_amdgcn_update_dpp(0, qv, 0x111, 0xF, 0xF, true);  // row_shr:1, q_{m-1}
+            sh = m ? sh : 0;
+            qv = l == i ? qv : (sh ^ pr);
         }
-        if (lane <= e)
-            lam[lane] = lm;
-        const uint8_t ai = lane < e ? aa[lane] : 0;
-        int lw = 0;  // log w_i, w_i = prod_{l != i} (a_i + a_l)
-        for (int l = 0; l < e; ++l)
-            if (l != lane)
-                lw += glog[ai ^ aa[l]];
-        lw %= 255;
-        if (lane < e)
-            lws[lane] = (uint8_t)lw;
-        lds_sync();
-        if (lane < e) {  // row i of V_E^-1 by synthetic division: the parity sources q = nl + m
-            uint8_t qm = lam[e];
-            for (int m = e - 1; m >= 0; --m) {
-                coef[lane * k + nl + m] = qm ? gexp[(glog[qm] + 255 - lw) % 255] : (uint8_t)0;
-                if (m)
-                    qm = lam[m] ^ gmul(ai, qm);
-            }
-        }
-        if (lane < nl) {  // survivor q: Lambda(b_q) / ((b_q + a_i) w_i)
-            const uint8_t bq = gexp[lv[lane]];
-            int lb = 0;
-            for (int l = 0; l < e; ++l)
-                lb += glog[bq ^ aa[l]];
-            lb %= 255;
-            for (int i = 0; i < e; ++i)
-                coef[i * k + lane] = gexp[(lb + 2 * 255 - glog[bq ^ aa[i]] - lws[i]) % 255];
-        }
+        if (i < e && m < e && nl + m >= j0 && nl + m < j1)
+            coef[i * k + nl + m] = qv ? gexp[(glog[qv] + 255 - log_w(i)) % 255] : 0;
     }
-    __syncthreads();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // own coefficients, read back below
+    tp.mark(2);
     if (blockIdx.x == 0 && threadIdx.x == 0)
         a.status[b] = 0;
     const uint32_t m4 = vconst(0x0F0F0F0Fu), m2 = vconst(0x33333333u), m1 = vconst(0x55555555u);
@@ -480,6 +512,7 @@ __global__ __launch_bounds__(64 * SPL) __attribute__((amdgpu_num_vgpr(64))) void
             mine[(t * 2 + 1) * 64 + lane] = make_uint4(W[4], W[5], W[6], W[7]);
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        tp.mark(3);
         const uint32_t la = base + lane * 16;
 #define RSGPU_TC_RUNV(N)                                                                          \
     asm volatile(RSGPU_TC_CHUNKV##N                                                               \
@@ -495,6 +528,7 @@ __global__ __launch_bounds__(64 * SPL) __attribute__((amdgpu_num_vgpr(64))) void
 #undef RSGPU_TC_RUNV
         // the next group reuses this wave's part and av
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        tp.mark(4);
     }
     uint32_t* part = reinterpret_cast<uint32_t*>(mine);
     [&]<int... Ss>(std::integer_sequence<int, Ss...>) {
@@ -511,6 +545,7 @@ __global__ __launch_bounds__(64 * SPL) __attribute__((amdgpu_num_vgpr(64))) void
             ...);
     }(std::make_integer_sequence<int, 8>{});
     __syncthreads();
+    tp.mark(5);
     if (off + 32 > a.len)
         return;
     for (int r = wave; r < e; r += SPL) {
@@ -525,6 +560,8 @@ __global__ __launch_bounds__(64 * SPL) __attribute__((amdgpu_num_vgpr(64))) void
         tr8(W, m4, m2, m1);
         store32(a.out + ((size_t)b * e + r) * a.pitch, off, W);
     }
+    tp.mark(6);
+    tp.end(lane);
 }
 
 }  // namespace tc

@@ -84,3 +84,18 @@ def test_survivor_runs_cover_exactly_the_live_rows(k, e, blocks, chunk):
             live[np.asarray(err[blk], np.int64)] = False
             want[blk * k:(blk + 1) * k] = live
         assert (got == want).all()
+
+
+def test_every_timed_kernel_has_algorithmic_bytes():
+    """Each kernel the C-ABI times under an (encode)/(decode) name is priced
+    in bench.alg_bytes: an unpriced one would print alg_GBps 0 and a zero
+    roofline when it is the step's dominant kernel."""
+    import re
+
+    import bench
+    src = open(os.path.join(ROOT, "storage-benchmarks_amd", "csrc", "rsgpu_capi.cpp")).read()
+    names = set(re.findall(r'"(k_[a-z0-9_]+\((?:encode|decode)\))"', src))
+    assert names, "no timed kernels found"
+    priced = bench.alg_bytes(16, 4, 1000)
+    missing = sorted(n for n in names if priced.get(n, 0.0) <= 0.0)
+    assert not missing, missing
