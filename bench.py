@@ -73,6 +73,7 @@ def parse(argv=None):
     p.add_argument("--encode-kernel", default="auto",
                    choices=["auto", "compiled", "generated", "threaded"])
     p.add_argument("--jitw-tiles", type=int, default=0, help=argparse.SUPPRESS)  # A/B hook
+    p.add_argument("--jitw-prefetch", type=int, default=-1, help=argparse.SUPPRESS)  # A/B hook
     # diagnostic: c4 batches from the third on keep the sources of two batches
     # before (verification still checks every batch against its buffer)
     p.add_argument("--no-regen", action="store_true", help=argparse.SUPPRESS)
@@ -611,6 +612,11 @@ def main(argv=None):
         f = rsgpu.lib().rsgpu_internal_set_jitw_tiles
         f.argtypes = [ctypes.c_void_p, ctypes.c_int]
         assert f(ctx._h, args.jitw_tiles) == 0
+    if args.jitw_prefetch >= 0:
+        import ctypes
+        f = rsgpu.lib().rsgpu_internal_set_jitw_prefetch
+        f.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        assert f(ctx._h, args.jitw_prefetch) == 0
     alg = alg_bytes(k, e, L)
     rank_info = None
 

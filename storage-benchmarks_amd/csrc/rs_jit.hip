@@ -275,6 +275,7 @@ __global__ __launch_bounds__(128 * TPW) __attribute__((amdgpu_num_vgpr(40))) voi
         b = (int)(lin / gridDim.x);
         tile = lin - (unsigned)b * gridDim.x;
     }
+    const long long wg = tile;  // this workgroup's index within its block
     tile = tile * TPW + tw;
     if (a.status && a.status[b] != 0)
         return;
@@ -302,6 +303,19 @@ __global__ __launch_bounds__(128 * TPW) __attribute__((amdgpu_num_vgpr(40))) voi
     else
         asm volatile(RSGPU_J10_ZERO ::: RSGPU_J10_ACC_CLOBBERS);
     issue(0);
+    if (a.code_prefetch) {
+        // the block's workgroups split its code (both row halves) and pull
+        // it into L2 with vector loads, every line in flight at once, so the
+        // instruction fetch, which misses line by line, finds it there; the
+        // wait also covers the sources just issued, needed next anyway
+        const uint8_t* cb = a.code + (size_t)b * a.block_stride;
+        const long long lines = (2LL * nch * a.chunk_stride) >> 7;
+        const long long lo = wg * lines / gridDim.x, hi = (wg + 1) * lines / gridDim.x;
+        for (long long i = lo + threadIdx.x; i < hi; i += 128 * TPW) {
+            uint32_t d;
+            asm volatile("global_load_dword %0, %1, off\n s_waitcnt vmcnt(0)" : "=v"(d) : "v"(cb + (i << 7)) : "memory");
+        }
+    }
     for (int ch = 0; ch < nch; ++ch) {
         const int nt = min(CS, k - ch * CS);
         uint4* buf = lds[ch & 1][tw];

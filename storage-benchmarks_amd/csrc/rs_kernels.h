@@ -102,6 +102,7 @@ struct JitArgs {
     const int* status;               // [B] or nullptr (every block runs)
     int xcd_order;                   // non-zero: XCD-contiguous (block, tile) order
     int tiles_per_wg = 1;            // k_rs_jitw: column tiles per workgroup (1, 2 or 3)
+    int code_prefetch = 0;           // k_rs_jitw: workgroups pull their block's code into L2 first
 };
 size_t jit_code_bytes(int k, int e, long long blocks);
 // k_rs_jit's straight-line code (rs_jit.h) for every (block, wave, chunk) at

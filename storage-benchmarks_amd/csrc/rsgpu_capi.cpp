@@ -1098,6 +1098,15 @@ int jit_decode_launch(rsgpu_ctx* ctx, int k, int e, size_t len, size_t blocks, c
         // blocks, C3 23.2-23.3 vs 23.4-23.5, C5 12.7-12.8 vs 12.8-12.9;
         // three tiles: 20-30 % slower; profiles/r03_ab/tpw/)
         j.tiles_per_wg = ctx->jitw_tpw ? ctx->jitw_tpw : 2;
+        // short rows: the block's few workgroups pull its code into L2 before
+        // the instruction fetch misses on it line by line (C4: 12.8 vs 13.7
+        // ms per 16384 blocks; C3, 245 workgroups per block, unchanged:
+        // profiles/r03_ab/prefetch/)
+        {
+            const long long wgs = ((long long)((len + 2047) / 2048) + j.tiles_per_wg - 1) / j.tiles_per_wg;
+            const long long lines = (long long)jitw_code_bytes(k, e, 1) / 128;
+            j.code_prefetch = ctx->jitw_prefetch >= 0 ? ctx->jitw_prefetch : lines >= 32 * wgs;
+        }
         KTimer kt(ctx,
                   jitw_rows(e) == 16   ? "k_rs_jit16(decode)"
                   : jitw_rows(e) == 12 ? "k_rs_jit12(decode)"
@@ -1456,6 +1465,16 @@ int rsgpu_internal_set_jitw_tiles(rsgpu_ctx* ctx, int n)
     if (!ctx || n < 0 || n > 3)
         return RSGPU_ERR_ARG;
     ctx->jitw_tpw = n;
+    return RSGPU_OK;
+}
+
+// A-B hook (not part of include/rsgpu.h): k_rs_jitw's code prefetch into L2
+// (0 off, 1 on, -1 the library's choice).
+int rsgpu_internal_set_jitw_prefetch(rsgpu_ctx* ctx, int n)
+{
+    if (!ctx || n < -1 || n > 1)
+        return RSGPU_ERR_ARG;
+    ctx->jitw_prefetch = n;
     return RSGPU_OK;
 }
 

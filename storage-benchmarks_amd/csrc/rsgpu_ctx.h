@@ -26,6 +26,7 @@ struct rsgpu_ctx {
     int tc_state = 0;
     int decode_kernel = RSGPU_DECODE_AUTO;
     int jitw_tpw = 0;  // k_rs_jitw column tiles per workgroup (0: by geometry)
+    int jitw_prefetch = -1;  // k_rs_jitw code prefetch into L2 (-1: by geometry)
     // executable device memory for the generated decode code (rs_jit.h):
     // grow-only; jit_state 0 = not probed, 1 = pool found, -1 = unavailable
     void* d_jit = nullptr;

@@ -654,3 +654,26 @@ def test_jitw_tiles_per_workgroup(ctx, tpw, k, e, L, B):
     finally:
         f(ctx._h, 0)
         ctx.set_decode_kernel("auto")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k,e,L,B", [(64, 32, 1000000, 2), (64, 32, 32000, 9), (100, 20, 6144, 3),
+                                     (48, 24, 14336, 2), (64, 17, 2048, 5)])
+def test_jitw_code_prefetch(ctx, k, e, L, B):
+    """k_rs_jitw with its workgroups pulling the block's code into L2 first
+    (the A/B hook rsgpu_internal_set_jitw_prefetch): the same recovered bytes
+    with the erased rows poisoned, for block-code sizes that leave some
+    workgroups no line to fetch (one tile per block)."""
+    import ctypes
+    f = rsgpu.lib().rsgpu_internal_set_jitw_prefetch
+    f.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    ctx.set_decode_kernel("generated")
+    assert f(ctx._h, 1) == 0
+    try:
+        enc = rsgpu.GpuEncoder(k, L, e, blocks=B, seed=73, ctx=ctx)
+        enc.encode_all()
+        dec = rsgpu.GpuDecoder(k, L, e, blocks=B, seed=73, ctx=ctx)
+        assert decode_poisoned(ctx, enc, dec)
+    finally:
+        f(ctx._h, -1)
+        ctx.set_decode_kernel("auto")
