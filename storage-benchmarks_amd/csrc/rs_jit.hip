@@ -290,11 +290,27 @@ __global__ __launch_bounds__(128 * TPW) __attribute__((amdgpu_num_vgpr(40))) voi
     const uint32_t loff = off + 32 <= a.len ? (uint32_t)off : 0u;  // tiles past the row re-read its head
     if (wv == 0)
         asm volatile("s_icache_inv\n s_nop 15\n s_nop 15" ::: "memory");
-    auto issue = [&](int ch) {
+    // the row pointers through the constant address space: scalar loads the
+    // compiler issues together and waits for once, a chunk ahead of their
+    // use (one s_load + wait per source measured 5-7 % of the wave's time)
+    typedef const uint8_t* const __attribute__((address_space(4)))* CPtrs;
+    const CPtrs csrcs = (CPtrs)srcs;
+    constexpr int PW = (CS + 1) / 2;  // this wave's sources per chunk: t = wave, wave + 2, ...
+    auto ptrs = [&](int ch, const uint8_t* (&p)[PW]) {
+        const int c0 = ch * CS, nt = min(CS, k - c0);
+#pragma unroll
+        for (int i = 0; i < PW; ++i)
+            p[i] = csrcs[c0 + min(wave + 2 * i, nt - 1)];  // in bounds, unconditional
+    };
+    auto issue = [&](int ch, const uint8_t* const (&p)[PW]) {
         const int c0 = ch * CS, nt = min(CS, k - c0);
         const uint32_t base = lds0 + (uint32_t)((ch & 1) * kBuf);
-        for (int t = wave; t < nt; t += 2)
-            glds32(sload_ptr(srcs + c0 + t), loff, base + (uint32_t)(t * 2 * 64 * 16));
+#pragma unroll
+        for (int i = 0; i < PW; ++i) {
+            const int t = wave + 2 * i;
+            if (t < nt)
+                glds32(p[i], loff, base + (uint32_t)(t * 2 * 64 * 16));
+        }
     };
     if constexpr (R == 16)
         asm volatile(RSGPU_J16_ZERO ::: RSGPU_J16_ACC_CLOBBERS);
@@ -302,7 +318,11 @@ __global__ __launch_bounds__(128 * TPW) __attribute__((amdgpu_num_vgpr(40))) voi
         asm volatile(RSGPU_J12_ZERO ::: RSGPU_J12_ACC_CLOBBERS);
     else
         asm volatile(RSGPU_J10_ZERO ::: RSGPU_J10_ACC_CLOBBERS);
-    issue(0);
+    const uint8_t* pc[PW];
+    const uint8_t* pn[PW];
+    ptrs(0, pc);
+    issue(0, pc);
+    ptrs(min(1, nch - 1), pn);
     if (a.code_prefetch) {
         // the block's workgroups split its code (both row halves) and pull
         // it into L2 with vector loads, every line in flight at once, so the
@@ -332,7 +352,8 @@ __global__ __launch_bounds__(128 * TPW) __attribute__((amdgpu_num_vgpr(40))) voi
         }
         barrier_lds();
         if (ch + 1 < nch)
-            issue(ch + 1);
+            issue(ch + 1, pn);
+        ptrs(min(ch + 2, nch - 1), pn);  // in flight during this chunk's code
         const uint32_t la = lds0 + (uint32_t)((ch & 1) * kBuf) + lane * 16;
         const uint8_t* fn = code + (size_t)ch * a.chunk_stride;
         if constexpr (R == 16)
@@ -351,6 +372,12 @@ __global__ __launch_bounds__(128 * TPW) __attribute__((amdgpu_num_vgpr(40))) voi
                          : [fn] "s"(fn), "{v9}"(la)
                          : RSGPU_JW_CALL_CLOBBERS, "s82", "s83", "scc", "memory", RSGPU_J10_ACC_CLOBBERS);
     }
+    // the output pointers likewise: all R loads under one wait
+    typedef uint8_t* const __attribute__((address_space(4)))* CDsts;
+    uint8_t* dp[R];
+#pragma unroll
+    for (int i = 0; i < R; ++i)
+        dp[i] = ((CDsts)dsts)[min(wave * R + i, a.rows - 1)];
     if (off + 32 <= a.len) {
         const uint32_t m4 = vconst(0x0F0F0F0Fu), m2 = vconst(0x33333333u), m1 = vconst(0x55555555u);
         [&]<int... Ss>(std::integer_sequence<int, Ss...>) {
@@ -361,7 +388,7 @@ __global__ __launch_bounds__(128 * TPW) __attribute__((amdgpu_num_vgpr(40))) voi
                         uint32_t Wd[8];
                         read_slotw<Ss>(Wd);
                         tr8(Wd, m4, m2, m1);
-                        store32((uint8_t*)sload_ptr((const uint8_t* const*)(dsts + r)), off, Wd);
+                        store32(dp[Ss], off, Wd);
                     }
                 }(),
                 ...);
