@@ -399,6 +399,18 @@ def test_bench_c4_streams_ragged_batches():
     assert "blocks=2500" in line["config"]["workload"]
 
 
+def test_bench_c2_line_prices_its_kernels():
+    """The C2 line (one block: split encode + one-launch decode): verified,
+    its roofline kernel the one-launch decode, every timed kernel priced
+    (a kernel missing from bench.alg_bytes used to report 0 GB/s)."""
+    line = run_bench(["--config", "c2", "--steps", "20", "--warmup", "2", "--no-cpu-baseline"])
+    assert line["verified"]
+    assert set(line["kernels"]) == {"k_rs_bs_split(encode)", "k_rs_tc_fused(decode)"}
+    assert all(v["alg_GBps"] > 0 for v in line["kernels"].values())
+    rf = line["roofline"]
+    assert rf["kernel"] == "k_rs_tc_fused(decode)" and rf["achieved"] > 0 and 0 < rf["frac"] < 1
+
+
 @pytest.mark.parametrize("kernel", ["auto", "generated", "one_matrix"])
 def test_batch_beyond_grid_limit(ctx, orc, kernel):
     """70000 blocks in one call (more than the 65535 a grid dimension holds):
@@ -602,7 +614,8 @@ def test_host_resident_api_poisoned(ctx, orc, k, e, L, B):
 
 
 @pytest.mark.parametrize("k,e,L,B", [(16, 4, 1000000, 1), (16, 8, 64000, 3), (64, 8, 100000, 2), (3, 1, 4096, 4),
-                                     (5, 4, 2080, 7), (40, 7, 6144, 5), (8, 8, 2048, 1)])
+                                     (5, 4, 2080, 7), (40, 7, 6144, 5), (8, 8, 2048, 1), (2, 2, 2048, 3),
+                                     (64, 1, 32768, 2), (33, 5, 4096, 3)])
 def test_fused_small_decode(ctx, orc, k, e, L, B):
     """The one-launch small-batch decode (k_rs_tc_fused): decode rows in
     closed form inside the kernel, sources split over four waves, partial
