@@ -373,6 +373,25 @@ def cpu_baseline(k, e, L, threads, kernel=1, blocks_per_thread=None, one_thread_
             "threads_1": one, "threads_nproc": many}
 
 
+def launch_cost(torch, n=400):
+    """Per-launch overhead on the engine's stream: n back-to-back launches
+    of a near-empty kernel (torch.cuda._sleep of one cycle), timed on the
+    device (HIP events: the gap between consecutive dispatches) and on the
+    host (enqueue + drain)."""
+    torch.cuda._sleep(1)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record()
+    for _ in range(n):
+        torch.cuda._sleep(1)
+    e1.record()
+    torch.cuda.synchronize()
+    host = time.perf_counter() - t0
+    return {"empty_kernel_us_device": round(e0.elapsed_time(e1) * 1e3 / n, 3),
+            "empty_kernel_us_host": round(host * 1e6 / n, 3)}
+
+
 def kernel_stats(recs, steps, alg):
     per, each = {}, {}
     for name, ms, nb in recs:
@@ -715,7 +734,10 @@ def main(argv=None):
         ms_step = elapsed / steps * 1e3
         workload = (f"isa_throughput {args.config}{' (custom geometry)' if custom else ''}: symbols={k} symbol_size={L} loss_rate={loss} "
                     f"erased={e} blocks_per_gpu={B}")
-        extra = {}
+        # launches per step and what one launch costs on this stream (short
+        # steps: C2's two launches)
+        extra = {"launch": dict(launch_cost(torch), launches_per_step=round(len(recs) / steps, 2),
+                                step_us=round(ms_step * 1e3, 2))}
 
     per, kernels = kernel_stats(recs, steps, alg)
     # dominant kernel = the most device time per step

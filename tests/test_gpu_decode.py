@@ -409,6 +409,8 @@ def test_bench_c2_line_prices_its_kernels():
     assert all(v["alg_GBps"] > 0 for v in line["kernels"].values())
     rf = line["roofline"]
     assert rf["kernel"] == "k_rs_tc_fused(decode)" and rf["achieved"] > 0 and 0 < rf["frac"] < 1
+    la = line["launch"]  # one launch per op, and what a launch costs on the stream
+    assert la["launches_per_step"] == 2 and la["empty_kernel_us_device"] > 0 and la["step_us"] > 0
 
 
 @pytest.mark.parametrize("kernel", ["auto", "generated", "one_matrix"])
