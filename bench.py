@@ -77,6 +77,9 @@ def parse(argv=None):
     # diagnostic: c4 batches from the third on keep the sources of two batches
     # before (verification still checks every batch against its buffer)
     p.add_argument("--no-regen", action="store_true", help=argparse.SUPPRESS)
+    # diagnostic: c4 generation of batch i+1 beside the verification of batch i
+    # (round-3 order) instead of after it
+    p.add_argument("--overlap-gen", action="store_true", help=argparse.SUPPRESS)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-threads", type=int, default=None)
     p.add_argument("--no-ref-base", action="store_true",
@@ -510,9 +513,14 @@ def run_streamed(args, rsgpu, ctx, dev, rank, world, k, e, L, total_blocks):
     erasure lists (global block index) uploaded on the `gen` stream; encode +
     decode (the timed regions, HIP events) and the device verify on the
     compute stream.
-    Batch i+1's generation waits for batch i's decode, so it overlaps only
-    the verification and the timed kernels run alone.  Returns (timed
-    seconds, wall seconds, mismatching bytes, batches, kernel records)."""
+    Each batch runs in the reference's order (isa.cpp / throughput_benchmark:
+    setup() fills the blocks, encode_all, decode_all, verify_data): batch
+    i+1's generation waits for batch i's verification, and the timed kernels
+    run alone.  (Generating batch i+1 beside batch i's verification, the
+    round-3 order kept behind --overlap-gen, shortens the wall time but left
+    the encode that follows a verification 1.0-1.4 ms slower per batch,
+    profiles/r03_ab/verify/.)  Returns (timed seconds, wall seconds,
+    mismatching bytes, batches, kernel records)."""
     import numpy as np
     import torch
     blk_base, share = split(total_blocks, rank, world)
@@ -544,9 +552,9 @@ def run_streamed(args, rsgpu, ctx, dev, rank, world, k, e, L, total_blocks):
         h_err[i & 1][:nb] = torch.from_numpy(rsgpu.erasure_patterns(args.seed, b0, nb, k, e))
         with torch.cuda.stream(s_gen):
             if i >= 1:
-                # after batch i-1's decode: generation overlaps only its
-                # verification, never the timed encode / decode kernels
-                s_gen.wait_event(ev_t[i - 1][1])
+                # after batch i-1's verification (--overlap-gen: its decode);
+                # never beside the timed encode / decode kernels
+                s_gen.wait_event(ev_t[i - 1][1] if args.overlap_gen else ev_done[i - 1])
             if i >= 2:
                 s_gen.wait_event(ev_done[i - 2])  # batch i-2 (same buffers) verified
             if i < 2 or not args.no_regen:
@@ -571,7 +579,7 @@ def run_streamed(args, rsgpu, ctx, dev, rank, world, k, e, L, total_blocks):
         ctx.decode_blocks(k, e, L, enc.pitch, nb, enc.src, enc.par, dec.err, dec.out, dec.ws,
                           dec.status)
         ev_t[i][1].record(s_cmp)
-        if i + 1 < nb_total:
+        if i + 1 < nb_total and args.overlap_gen:
             generate(i + 1)
         if not args.no_verify:
             ctx.verify_blocks(k, e, L, enc.pitch, nb, enc.src, dec.out, dec.err, dec.mism)
@@ -581,14 +589,19 @@ def run_streamed(args, rsgpu, ctx, dev, rank, world, k, e, L, total_blocks):
                 mism[i:i + 1].copy_(bad.view(1))
                 dec.mism.zero_()
         ev_done[i].record(s_cmp)
+        if i + 1 < nb_total and not args.overlap_gen:
+            generate(i + 1)
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
-    timed = sum(a.elapsed_time(b) for a, b in ev_t) * 1e-3
+    per_batch = [a.elapsed_time(b) for a, b in ev_t]
+    timed = sum(per_batch) * 1e-3
     recs = ctx.timing_read()
     ctx.timing_enable(False)
     ctx.set_torch_stream()
     gen_ctx.close()
-    return timed, wall, int(mism.sum().item()), nb_total, batch, recs
+    q = sorted(per_batch)
+    batch_ms = {"min": round(q[0], 3), "median": round(statistics.median(q), 3), "max": round(q[-1], 3)}
+    return timed, wall, int(mism.sum().item()), nb_total, batch, recs, batch_ms
 
 
 def main(argv=None):
@@ -647,7 +660,7 @@ def main(argv=None):
             w_dec.decode_all(w_enc)
             torch.cuda.synchronize()
             del w_enc, w_dec
-        timed, wall, bad, nbatches, batch, recs = run_streamed(args, rsgpu, ctx, dev, rank, world,
+        timed, wall, bad, nbatches, batch, recs, batch_ms = run_streamed(args, rsgpu, ctx, dev, rank, world,
                                                                k, e, L, B)
         blk0, share = split(B, rank, world)
         if world > 1:
@@ -671,6 +684,7 @@ def main(argv=None):
         extra = {"streamed": {"blocks_total": B, "blocks_per_gpu": B / world, "blocks_rank0": share,
                               "batches": nbatches,
                               "batch_blocks": batch, "timed_s": elapsed, "wall_s": wall,
+                              "batch_ms_rank0": batch_ms,
                               "wall_GiBps": 2.0 * e * L * B / wall / 2 ** 30,
                               "mismatch_bytes": bad_t.item(),
                               "note": "value: encode+decode regions (HIP events) summed over "

@@ -23,37 +23,46 @@ __device__ __forceinline__ uint32_t vconst(uint32_t c)
     return v;
 }
 
-// (lo, hi) block swap of the SWAR 8x8 bit transpose, per byte lane:
-//   lo' = (lo & m) | ((hi << s) & ~m),  hi' = ((lo >> s) & m) | (hi & ~m)
-// bitop3 truth tables (src0=0xF0, src1=0xCC, src2=0xAA):
+// Two (lo, hi) block swaps of the SWAR 8x8 bit transpose at once, per byte
+// lane:  lo' = (lo & m) | ((hi << s) & ~m),  hi' = ((lo >> s) & m) | (hi & ~m)
+// for (lo0, hi0) and (lo1, hi1).  The two lo are shifted as ONE 64-bit value
+// (lo1:lo0) >> s, the two hi as (hi1:hi0) << s: the s bits that cross the
+// dword boundary land at the top of lo0 >> s / the bottom of hi1 << s, where
+// m (0x0F0F0F0F, 0x33333333, 0x55555555 for s = 4, 2, 1) selects the other
+// operand, so they never reach a result.  12 shifts per tr8 instead of 24
+// (hipcc splits a C++ 64-bit shift whose halves are used separately into
+// v_alignbit + v_lshrrev, hence the asm; it pairs the operands in aligned
+// VGPR pairs without a move, tools/tr8_codegen: 24 v_bitop3 + 12 64-bit shifts).
+// bitop3 truth table (src0=0xF0, src1=0xCC, src2=0xAA):
 //   f(a, b, m) = (a & m) | (b & ~m)  -> (0xF0 & 0xAA) | (0xCC & 0x55) = 0xE4
 template <int S>
-__device__ __forceinline__ void swap_blk(uint32_t& lo, uint32_t& hi, uint32_t m)
+__device__ __forceinline__ void swap_blk2(uint32_t& lo0, uint32_t& lo1, uint32_t& hi0, uint32_t& hi1, uint32_t m)
 {
-    const uint32_t hs = hi << S;
-    const uint32_t ls = lo >> S;
-    const uint32_t nl = __builtin_amdgcn_bitop3_b32(lo, hs, m, 0xE4);
-    const uint32_t nh = __builtin_amdgcn_bitop3_b32(ls, hi, m, 0xE4);
-    lo = nl;
-    hi = nh;
+    uint64_t l, h;
+    asm("v_lshrrev_b64 %0, %1, %2" : "=v"(l) : "i"(S), "v"((uint64_t)lo1 << 32 | lo0));
+    asm("v_lshlrev_b64 %0, %1, %2" : "=v"(h) : "i"(S), "v"((uint64_t)hi1 << 32 | hi0));
+    const uint32_t nl0 = __builtin_amdgcn_bitop3_b32(lo0, (uint32_t)h, m, 0xE4);
+    const uint32_t nl1 = __builtin_amdgcn_bitop3_b32(lo1, (uint32_t)(h >> 32), m, 0xE4);
+    const uint32_t nh0 = __builtin_amdgcn_bitop3_b32((uint32_t)l, hi0, m, 0xE4);
+    const uint32_t nh1 = __builtin_amdgcn_bitop3_b32((uint32_t)(l >> 32), hi1, m, 0xE4);
+    lo0 = nl0;
+    lo1 = nl1;
+    hi0 = nh0;
+    hi1 = nh1;
 }
 
 // In place: W[w] byte q = byte (4w+q) of a 32-byte segment  <->  plane
-// layout W[a] byte q bit w = bit a of that byte.  Self-inverse.
+// layout W[a] byte q bit w = bit a of that byte.  Self-inverse.  Block swaps
+// (0,4)(1,5)(2,6)(3,7) by 4 bits, (0,2)(1,3)(4,6)(5,7) by 2, (0,1)(2,3)(4,5)(6,7)
+// by 1, grouped in pairs whose lo (and hi) halves are shifted together.
 __device__ __forceinline__ void tr8(uint32_t (&W)[8], uint32_t m4, uint32_t m2, uint32_t m1)
 {
-    swap_blk<4>(W[0], W[4], m4);
-    swap_blk<4>(W[1], W[5], m4);
-    swap_blk<4>(W[2], W[6], m4);
-    swap_blk<4>(W[3], W[7], m4);
-    swap_blk<2>(W[0], W[2], m2);
-    swap_blk<2>(W[1], W[3], m2);
-    swap_blk<2>(W[4], W[6], m2);
-    swap_blk<2>(W[5], W[7], m2);
-    swap_blk<1>(W[0], W[1], m1);
-    swap_blk<1>(W[2], W[3], m1);
-    swap_blk<1>(W[4], W[5], m1);
-    swap_blk<1>(W[6], W[7], m1);
+    swap_blk2<4>(W[0], W[1], W[4], W[5], m4);
+    swap_blk2<4>(W[2], W[3], W[6], W[7], m4);
+    swap_blk2<2>(W[0], W[1], W[2], W[3], m2);
+    swap_blk2<2>(W[4], W[5], W[6], W[7], m2);
+    swap_blk2<1>(W[0], W[2], W[1], W[3], m1);
+    swap_blk2<1>(W[4], W[6], W[5], W[7], m1);
 }
 
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));

@@ -74,33 +74,34 @@ RJ_HD constexpr int table_reg(int bank, int hi, int n)
 
 // ---- gfx950 encodings (llvm-mc -mcpu=gfx950 -show-encoding) -------------
 
-RJ_HD inline uint64_t enc_bitop3_96(int d, int a, int b, int c)  // d = a ^ b ^ c
+RJ_HD constexpr uint64_t enc_bitop3_96(int d, int a, int b, int c)  // d = a ^ b ^ c
 {
     const uint32_t w0 = 0xd2340200u | (uint32_t)d;
     const uint32_t w1 = 0xd0000000u | ((uint32_t)(256 + c) << 18) | ((uint32_t)(256 + b) << 9) |
                         (uint32_t)(256 + a);
     return (uint64_t)w1 << 32 | w0;
 }
-RJ_HD inline uint64_t enc_xor_e64(int d, int a, int b)  // VOP3 form, 8 bytes
+RJ_HD constexpr uint64_t enc_xor_e64(int d, int a, int b)  // VOP3 form, 8 bytes
 {
     const uint32_t w0 = 0xd1150000u | (uint32_t)d;
     const uint32_t w1 = ((uint32_t)(256 + b) << 9) | (uint32_t)(256 + a);
     return (uint64_t)w1 << 32 | w0;
 }
-RJ_HD inline uint32_t enc_xor_e32(int d, int a, int b)  // VOP2, 4 bytes
+RJ_HD constexpr uint32_t enc_xor_e32(int d, int a, int b)  // VOP2, 4 bytes
 {
     return 0x2a000000u | ((uint32_t)d << 17) | ((uint32_t)b << 9) | (uint32_t)(256 + a);
 }
-RJ_HD inline uint64_t enc_ds_read_b128(int vd, int vaddr, int offset)
+RJ_HD constexpr uint64_t enc_ds_read_b128(int vd, int vaddr, int offset)
 {
     return (uint64_t)(((uint32_t)vd << 24) | (uint32_t)vaddr) << 32 | (0xd9fe0000u | (uint32_t)offset);
 }
 constexpr uint32_t S_NOP0 = 0xbf800000u;
+constexpr uint64_t NOP2 = (uint64_t)S_NOP0 << 32 | S_NOP0;  // two s_nop 0: a zero-mask word
 constexpr uint32_t S_SETPC_82 = 0xbe801d52u;  // s_setpc_b64 s[82:83]
-RJ_HD inline uint32_t enc_waitcnt_lgkm(int n) { return 0xbf8cc07fu | ((uint32_t)n << 8); }
+RJ_HD constexpr uint32_t enc_waitcnt_lgkm(int n) { return 0xbf8cc07fu | ((uint32_t)n << 8); }
 
 // Row b of the 8 x 8 GF(2) matrix of x -> c x: bit a set iff bit b of c 2^a.
-RJ_HD inline uint8_t mat_row(uint8_t c, int b)
+RJ_HD constexpr uint8_t mat_row(uint8_t c, int b)
 {
     uint8_t x = c, r = 0;
     for (int a = 0; a < 8; ++a) {
@@ -215,7 +216,7 @@ struct Wide {
     RJ_HD static constexpr int src_bytes(int nslot) { return PRE + 64 * nslot; }
     RJ_HD static constexpr int chunk_stride() { return (CS * src_bytes(R) + 8 + 63) / 64 * 64; }
 
-    RJ_HD static int treg(int hi, int n)
+    RJ_HD static constexpr int treg(int hi, int n)
     {
         if ((n & (n - 1)) == 0) {
             const int a = n == 1 ? 0 : n == 2 ? 1 : n == 4 ? 2 : 3;
@@ -225,16 +226,28 @@ struct Wide {
         return CL + 11 * hi + (n - below - 1);
     }
 
+    // the multiply-accumulate word for mask m with the accumulator fields
+    // zero: acc ^= L[m & 15] ^ H[m >> 4] (v_bitop3_b32 0x96, or v_xor_b32 in
+    // the VOP3 form when one nibble is 0; an s_nop pair for m = 0).  The
+    // accumulator is both the destination (low byte of the first dword) and
+    // src0 (256 + acc, low 9 bits of the second), so for acc < 256 the word of
+    // accumulator acc is this base OR (acc << 32 | acc).
+    RJ_HD static constexpr uint64_t mac_base(uint8_t m)
+    {
+        const int lo = m & 15, hi = m >> 4;
+        return lo && hi ? enc_bitop3_96(0, 0, treg(0, lo), treg(1, hi))
+               : lo     ? enc_xor_e64(0, 0, treg(0, lo))
+               : hi     ? enc_xor_e64(0, 0, treg(1, hi))
+                        : NOP2;
+    }
+    RJ_HD static constexpr uint64_t with_acc(uint64_t base, int acc)
+    {
+        return base == NOP2 ? NOP2 : base | ((uint64_t)acc << 32 | (uint64_t)acc);
+    }
+
     // the multiply-accumulate word of output plane b of slot s, for row b
     // (mask m = mat_row(c, b)) of the coefficient's matrix
-    RJ_HD static uint64_t mac_word(uint8_t m, int s, int b)
-    {
-        const int acc = ACC + 8 * s + b, lo = m & 15, hi = m >> 4;
-        return lo && hi ? enc_bitop3_96(acc, acc, treg(0, lo), treg(1, hi))
-               : lo     ? enc_xor_e64(acc, acc, treg(0, lo))
-               : hi     ? enc_xor_e64(acc, acc, treg(1, hi))
-                        : (uint64_t)S_NOP0 << 32 | S_NOP0;
-    }
+    RJ_HD static constexpr uint64_t mac_word(uint8_t m, int s, int b) { return with_acc(mac_base(m), ACC + 8 * s + b); }
 
     RJ_HD static void mac_words(uint8_t c, int s, uint64_t (&wd)[8])
     {
@@ -243,7 +256,7 @@ struct Wide {
     }
 
     // 32-bit word i (< PRE / 4 = 28) of source t's preamble
-    RJ_HD static uint32_t pre_u32(int t, int i)
+    RJ_HD static constexpr uint32_t pre_u32(int t, int i)
     {
         if (i < 4) {
             const uint64_t d = enc_ds_read_b128(i < 2 ? PL : PL + 4, ADDR, t * LDS_SRC + (i < 2 ? 0 : LDS_HALF));
@@ -287,6 +300,26 @@ struct Wide {
 using J16 = Wide<16, 6>;
 using J12 = Wide<12, 6>;
 using J10 = Wide<10, 5>;
+
+// Word tables of the device emitter k_jitw_emit (the register contract, and
+// so every table, is the same for all R): the base word (mac_base) of
+// coefficient c for output plane b at [8 c + b], and the 14 preamble words
+// of chunk position t at [14 t + i / 2] (i = 0 .. 27 as pre_u32).
+struct WideTables {
+    uint64_t mac[256 * 8];
+    uint64_t pre[6 * 14];
+};
+RJ_HD constexpr WideTables wide_tables()
+{
+    WideTables w{};
+    for (int c = 0; c < 256; ++c)
+        for (int b = 0; b < 8; ++b)
+            w.mac[8 * c + b] = J16::mac_base(mat_row((uint8_t)c, b));
+    for (int t = 0; t < 6; ++t)
+        for (int r = 0; r < 14; ++r)
+            w.pre[14 * t + r] = (uint64_t)J16::pre_u32(t, 2 * r + 1) << 32 | J16::pre_u32(t, 2 * r);
+    return w;
+}
 
 }  // namespace jit
 }  // namespace rsgpu

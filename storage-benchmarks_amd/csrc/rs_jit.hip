@@ -461,15 +461,23 @@ __global__ __launch_bounds__(256) void k_jit_emit(int k, int e, const uint8_t* c
     }
 }
 
+// The word tables of k_jitw_emit (rs_jit.h wide_tables), built at compile time.
+__constant__ jit::WideTables kWideTab = jit::wide_tables();
+
 // k_rs_jitw<R>'s code (rs_jit.h Wide), one workgroup per (block, wave) as
-// k_jit_emit: rows R w .. R w + R - 1 of the block's decode rows
+// k_jit_emit: rows R w .. R w + R - 1 of the block's decode rows.  Each word
+// is a table entry (the coefficient's matrix row and register operands are
+// fixed per (c, plane)) with the accumulator ORed in: per 16 bytes of code
+// one 16-byte table load, two selects and ORs.  (Computing every word from
+// the coefficient's 8 x 8 matrix took ~3500 VALU + 2400 SALU per wave; the
+// emission of a C4 batch, 2.5 GB of code, 0.85-0.9 ms.)
 template <class W>
 __global__ __launch_bounds__(256) void k_jitw_emit(int k, int e, const uint8_t* coef, const int* status,
                                                    uint8_t* code)
 {
-    constexpr int R = W::R, CS = W::CS;
+    constexpr int R = W::R, CS = W::CS, PW = W::PRE / 8;
+    static_assert(PW == 14 && CS <= 6, "preamble table: 14 words per source, chunk positions < 6");
     __shared__ uint8_t cw[R * 256];
-    __shared__ uint8_t mrow[256 * 8];  // row b of the matrix of coefficient c at mrow[8 c + b]
     const int b = blockIdx.y, w = blockIdx.x;
     if (status[b] != 0)
         return;
@@ -480,39 +488,26 @@ __global__ __launch_bounds__(256) void k_jitw_emit(int k, int e, const uint8_t* 
     const int sb = W::src_bytes(nslot);
     for (int i = threadIdx.x; i < nslot * k; i += blockDim.x)
         cw[i] = coef[((size_t)b * e + R * w) * k + i];
-    {  // the 256 matrices once per workgroup: thread c, column a = c 2^a
-        const int c = threadIdx.x;
-        uint8_t x = (uint8_t)c, row[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        for (int a = 0; a < 8; ++a) {
-#pragma unroll
-            for (int bb = 0; bb < 8; ++bb)
-                row[bb] |= (uint8_t)(((x >> bb) & 1) << a);
-            x = (uint8_t)((x << 1) ^ ((x & 0x80) ? 0x1D : 0));
-        }
-#pragma unroll
-        for (int bb = 0; bb < 8; ++bb)
-            mrow[8 * c + bb] = row[bb];
-    }
     __syncthreads();
-    // (source, slot) runs of 64 bytes, one 16-byte quarter per thread, so a
-    // wave's store covers 1 KB of consecutive code
+    // (source, slot) runs of 64 bytes, one 16-byte quarter (planes 2j, 2j+1)
+    // per thread, so a wave's store covers 1 KB of consecutive code
     for (int i = threadIdx.x; i < R * k * 4; i += blockDim.x) {
         const int run = i >> 2, j = i & 3;
         const int q = run / R, s = run - q * R;
         if (s >= nslot)
             continue;
         const int ch = q / CS, t = q - ch * CS;
-        const uint8_t* mr = mrow + 8 * cw[s * k + q];
-        const uint64_t w0 = W::mac_word(mr[2 * j], s, 2 * j), w1 = W::mac_word(mr[2 * j + 1], s, 2 * j + 1);
+        const uint4 bw = *reinterpret_cast<const uint4*>(&kWideTab.mac[8 * cw[s * k + q] + 2 * j]);
+        const int acc = W::ACC + 8 * s + 2 * j;
+        const uint64_t w0 = W::with_acc((uint64_t)bw.y << 32 | bw.x, acc);
+        const uint64_t w1 = W::with_acc((uint64_t)bw.w << 32 | bw.z, acc + 1);
         reinterpret_cast<uint4*>(cbase + (size_t)ch * stride + (size_t)t * sb + W::PRE + 64 * s)[j] =
             make_uint4((uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1, (uint32_t)(w1 >> 32));
     }
-    constexpr int PW = W::PRE / 8;
     for (int i = threadIdx.x; i < PW * k; i += blockDim.x) {  // preambles
         const int q = i / PW, r = i - q * PW;
         const int ch = q / CS, t = q - ch * CS;
-        reinterpret_cast<uint64_t*>(cbase + (size_t)ch * stride + (size_t)t * sb)[r] =
-            (uint64_t)W::pre_u32(t, 2 * r + 1) << 32 | W::pre_u32(t, 2 * r);
+        reinterpret_cast<uint64_t*>(cbase + (size_t)ch * stride + (size_t)t * sb)[r] = kWideTab.pre[PW * t + r];
     }
     for (int ch = threadIdx.x; ch < nch; ch += blockDim.x) {  // returns
         const int nt = min(CS, k - CS * ch);

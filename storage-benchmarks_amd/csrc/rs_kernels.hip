@@ -31,6 +31,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
 #include <utility>
 
 #include "gf256.h"
@@ -593,23 +594,28 @@ __global__ __launch_bounds__(256) void k_decode_prepare(PrepArgs a)
 // Synthetic data and verification
 // ---------------------------------------------------------------------------
 
+// Rows over the grid's y dimension (grid-stride), 8-byte words over x: no
+// per-element 64-bit division (a flat index split by a runtime row length
+// cost ~130 VALU per word; the fill of a C4 batch took ~25 ms).
 __global__ __launch_bounds__(256) void k_fill_synth(uint8_t* __restrict__ dst, long long rows,
                                                     long long len, long long pitch,
                                                     unsigned long long seed,
                                                     unsigned long long row0)
 {
     const long long words = (len + 7) / 8;
-    const long long total = rows * words;
-    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
-         i += (long long)gridDim.x * blockDim.x) {
-        const long long r = i / words, w = i - r * words;
-        const uint64_t v = synth_word(seed, row0 + (uint64_t)r, (uint64_t)w);
-        uint8_t* p = dst + r * pitch + w * 8;
-        if (w * 8 + 8 <= len && ((reinterpret_cast<uintptr_t>(p) & 7) == 0)) {
-            *reinterpret_cast<uint64_t*>(p) = v;
-        } else {
-            for (int q = 0; q < 8 && w * 8 + q < len; ++q)
-                p[q] = (uint8_t)(v >> (8 * q));
+    const bool whole = (pitch % 8) == 0 && (reinterpret_cast<uintptr_t>(dst) & 7) == 0;
+    for (long long r = blockIdx.y; r < rows; r += gridDim.y) {
+        uint8_t* row = dst + r * pitch;
+        for (long long w = (long long)blockIdx.x * blockDim.x + threadIdx.x; w < words;
+             w += (long long)gridDim.x * blockDim.x) {
+            const uint64_t v = synth_word(seed, row0 + (uint64_t)r, (uint64_t)w);
+            uint8_t* p = row + w * 8;
+            if (whole && w * 8 + 8 <= len) {
+                *reinterpret_cast<uint64_t*>(p) = v;
+            } else {
+                for (int q = 0; q < 8 && w * 8 + q < len; ++q)
+                    p[q] = (uint8_t)(v >> (8 * q));
+            }
         }
     }
 }
@@ -634,7 +640,24 @@ __global__ __launch_bounds__(256) void k_compare_rows(const uint8_t* __restrict_
     }
     const uint8_t* s = src + ((size_t)b * k + sidx) * src_pitch;
     unsigned long long bad = 0;
-    for (long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x; p < len;
+    long long head = 0;  // bytes compared 16 at a time
+    if (((reinterpret_cast<uintptr_t>(o) | reinterpret_cast<uintptr_t>(s)) & 15) == 0) {
+        head = len & ~15LL;
+        for (long long p = ((long long)blockIdx.x * blockDim.x + threadIdx.x) * 16; p < head;
+             p += (long long)gridDim.x * blockDim.x * 16) {
+            const uint4 x = *reinterpret_cast<const uint4*>(o + p);
+            const uint4 y = *reinterpret_cast<const uint4*>(s + p);
+            const uint32_t d[4] = {x.x ^ y.x, x.y ^ y.y, x.z ^ y.z, x.w ^ y.w};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {  // differing bytes: a bit per nonzero byte of d
+                uint32_t t = d[q] | (d[q] >> 4);
+                t |= t >> 2;
+                t |= t >> 1;
+                bad += __builtin_popcount(t & 0x01010101u);
+            }
+        }
+    }
+    for (long long p = head + (long long)blockIdx.x * blockDim.x + threadIdx.x; p < len;
          p += (long long)gridDim.x * blockDim.x)
         bad += (o[p] != s[p]);
     // wave reduction then one atomic per wave
@@ -764,13 +787,11 @@ hipError_t launch_fill_synth(uint8_t* dst, long long rows, long long len, long l
                              unsigned long long seed, unsigned long long row0, hipStream_t st)
 {
     const long long words = (len + 7) / 8;
-    const long long total = rows * words;
-    long long want = (total + 255) / 256;
-    if (want > 65536)
-        want = 65536;
-    if (want < 1)
-        want = 1;
-    hipLaunchKernelGGL(k_fill_synth, dim3((unsigned)want), dim3(256), 0, st, dst, rows, len,
+    if (rows <= 0 || words <= 0)
+        return hipSuccess;
+    const long long gx = std::min<long long>((words + 255) / 256, 1024);
+    const long long gy = std::min<long long>(rows, 65535);
+    hipLaunchKernelGGL(k_fill_synth, dim3((unsigned)gx, (unsigned)gy), dim3(256), 0, st, dst, rows, len,
                        pitch, seed, row0);
     return hipGetLastError();
 }
@@ -779,11 +800,8 @@ hipError_t launch_compare_rows(const uint8_t* src, long long src_pitch, int k, c
                                long long out_pitch, int e, const uint8_t* err, long long len,
                                long long blocks, unsigned long long* mismatches, hipStream_t st)
 {
-    long long want = (len + 255) / 256;
-    if (want > 64)
-        want = 64;
-    if (want < 1)
-        want = 1;
+    // 16 bytes per lane: 4 KB per workgroup pass
+    const long long want = std::max<long long>(1, std::min<long long>((len + 4095) / 4096, 64));
     dim3 grid((unsigned)want, (unsigned)e, (unsigned)blocks);
     hipLaunchKernelGGL(k_compare_rows, grid, dim3(256), 0, st, src, src_pitch, k, out, out_pitch,
                        e, err, len, mismatches);

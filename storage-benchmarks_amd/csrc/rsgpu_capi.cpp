@@ -1454,10 +1454,6 @@ int rsgpu_fill_synthetic(rsgpu_ctx* ctx, unsigned char* d_rows, size_t rows, siz
     return RSGPU_OK;
 }
 
-// Test hook (not in include/rsgpu.h): the host-built code of an e x k matrix
-// shared by every block (jit_prog.h, the GENERATED encode), for the CPU
-// suite to disassemble and interpret.  Returns the bytes needed, or -1;
-// writes only when out_bytes is large enough; *chunk_stride gets the stride.
 // Test / A-B hook (not part of include/rsgpu.h): column tiles per workgroup
 // of the two-wave generated decode (1, 2, 3; 0 = the library's choice).
 int rsgpu_internal_set_jitw_tiles(rsgpu_ctx* ctx, int n)
@@ -1478,6 +1474,10 @@ int rsgpu_internal_set_jitw_prefetch(rsgpu_ctx* ctx, int n)
     return RSGPU_OK;
 }
 
+// Test hook (not in include/rsgpu.h): the host-built code of an e x k matrix
+// shared by every block (jit_prog.h, the GENERATED encode), for the CPU
+// suite to disassemble and interpret.  Returns the bytes needed, or -1;
+// writes only when out_bytes is large enough; *chunk_stride gets the stride.
 long long rsgpu_internal_jit_matrix_code(int k, int e, const unsigned char* coef, unsigned char* out,
                                          size_t out_bytes, int* chunk_stride, int max_ops)
 {
@@ -1557,6 +1557,37 @@ long long rsgpu_internal_jitw_emit(int k, int e, const unsigned char* coef, unsi
     else
         jitw_emit_host<jit::J10>(k, e, coef, o64);
     return (long long)need;
+}
+
+// Test hook (not part of include/rsgpu.h): the DEVICE emitter k_jitw_emit
+// for `blocks` blocks of decode rows coef [blocks][e][k] (host memory), its
+// code copied back into out (blocks x the bytes rsgpu_internal_jitw_emit
+// returns for one block), so a GPU test compares it word for word with the
+// host emitter the CPU suite interprets.  Returns the bytes, or -1.
+long long rsgpu_internal_jitw_emit_device(rsgpu_ctx* ctx, int k, int e, size_t blocks,
+                                          const unsigned char* coef, unsigned char* out, size_t out_bytes)
+{
+    if (!ctx || k <= 0 || !jitw_rows(e) || k + e > 250 || blocks == 0 || blocks > kMaxGridBlocks || !coef)
+        return -1;
+    const size_t need = jitw_code_bytes(k, e, (long long)blocks);
+    if (!out || out_bytes < need)
+        return (long long)need;
+    uint8_t *d_coef = nullptr, *d_code = nullptr;
+    int* d_status = nullptr;
+    long long rc = -1;
+    if (hipMalloc(&d_coef, blocks * e * k) == hipSuccess && hipMalloc(&d_code, need) == hipSuccess &&
+        hipMalloc(&d_status, blocks * sizeof(int)) == hipSuccess &&
+        hipMemcpyAsync(d_coef, coef, blocks * e * k, hipMemcpyHostToDevice, ctx->stream) == hipSuccess &&
+        hipMemsetAsync(d_status, 0, blocks * sizeof(int), ctx->stream) == hipSuccess &&
+        launch_jit_fill(d_code, need, ctx->stream) == hipSuccess &&
+        launch_jitw_emit(k, e, (long long)blocks, d_coef, d_status, d_code, ctx->stream) == hipSuccess &&
+        hipMemcpyAsync(out, d_code, need, hipMemcpyDeviceToHost, ctx->stream) == hipSuccess &&
+        hipStreamSynchronize(ctx->stream) == hipSuccess)
+        rc = (long long)need;
+    (void)hipFree(d_coef);
+    (void)hipFree(d_code);
+    (void)hipFree(d_status);
+    return rc;
 }
 
 int rsgpu_erasure_patterns(uint64_t seed, uint64_t blk0, size_t blocks, int k, int e,

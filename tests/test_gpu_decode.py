@@ -692,3 +692,32 @@ def test_jitw_code_prefetch(ctx, k, e, L, B):
     finally:
         f(ctx._h, -1)
         ctx.set_decode_kernel("auto")
+
+
+@pytest.mark.parametrize("k,e", [(64, 32), (25, 25), (218, 32), (48, 24), (21, 21), (100, 20), (17, 17),
+                                 (230, 20)])
+def test_device_emitter_writes_the_host_emitters_code(ctx, k, e):
+    """k_jitw_emit (table-driven, on the device) writes, block for block and
+    word for word, the code of the host emitter Wide::code_word, which the
+    CPU suite disassembles and interprets (tests/test_jit.py)."""
+    import ctypes as C
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from test_jit import emitw
+    rng = np.random.default_rng(k * 1000 + e)
+    blocks = 3
+    coef = rng.integers(0, 256, (blocks, e, k), dtype=np.uint8)
+    coef[0, 1, :5] = 0          # zero coefficients: s_nop pairs
+    coef[1, 0, :] = 1
+    coef[2, :, 0] = 0x80
+    f = rsgpu.lib().rsgpu_internal_jitw_emit_device
+    f.restype = C.c_longlong
+    f.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_size_t, C.c_void_p, C.c_void_p, C.c_size_t]
+    need = f(ctx._h, k, e, blocks, coef.ctypes.data, None, 0)
+    assert need > 0
+    out = np.zeros(need, np.uint8)
+    assert f(ctx._h, k, e, blocks, coef.ctypes.data, out.ctypes.data, need) == need
+    per = need // blocks
+    for b in range(blocks):
+        host = emitw(k, e, coef[b])
+        assert host.size == per
+        assert np.array_equal(out[b * per:(b + 1) * per], host), b

@@ -59,6 +59,49 @@ def test_fill_synthetic_matches_definition(ctx):
             assert (got[r, L:] == 0).all()
 
 
+def test_fill_synthetic_many_rows_and_odd_base(ctx):
+    """More rows than one grid dimension holds (the fill's row loop), and a
+    destination that is not 8-byte aligned (bytewise stores)."""
+    rows, L, pitch = 70000, 24, 32
+    buf = torch.zeros(rows * pitch + 8, dtype=torch.uint8, device="cuda")
+    ctx.fill_synthetic(buf, rows, L, pitch, 5, 3)
+    got = buf[:rows * pitch].view(rows, pitch).cpu().numpy()
+    for r in (0, 1, 65534, 65535, 65536, rows - 1):
+        assert (got[r, :L] == synth_row(5, 3 + r, L)).all()
+    odd = buf[1:]
+    ctx.fill_synthetic(odd, 3, 21, 29, 6, 0)
+    g = odd[:3 * 29].view(3, 29).cpu().numpy()
+    for r in range(3):
+        assert (g[r, :21] == synth_row(6, r, 21)).all()
+
+
+@pytest.mark.parametrize("L", [32000, 1000, 4099])
+def test_verify_counts_each_differing_byte(ctx, L):
+    """rsgpu_verify_blocks (isa.cpp:215-229 on the device) counts every
+    differing byte of a recovered row, in the 16-byte body and the tail."""
+    k, e, B = 8, 3, 4
+    pitch = (L + 255) // 256 * 256
+    rng = np.random.default_rng(L)
+    src = torch.from_numpy(rng.integers(0, 256, (B, k, pitch), dtype=np.uint8)).cuda()
+    err = np.array([[1, 4, 6]] * B, np.uint8)
+    out = src[:, [1, 4, 6], :].clone()
+    for b in range(1, B):
+        pos = rng.choice(L, size=5 * b, replace=False)
+        for p in pos:
+            r = int(rng.integers(0, e))
+            out[b, r, int(p)] ^= int(rng.integers(1, 256))
+        # several bytes of one dword, and the last byte
+        out[b, 0, 16:20] ^= 0xFF
+        out[b, 2, L - 1] ^= 1
+    # count what actually differs (a random position may repeat a fixed one)
+    ref = (out.cpu().numpy()[:, :, :L] != src.cpu().numpy()[:, [1, 4, 6], :L]).sum(axis=(1, 2))
+    mism = torch.zeros(B, dtype=torch.int64, device="cuda")
+    ctx.verify_blocks(k, e, L, pitch, B, src, out, dev(err), mism)
+    torch.cuda.synchronize()
+    assert mism.cpu().numpy().tolist() == ref.tolist()
+    assert int(mism[0]) == 0 and (ref[1:] > 0).all()
+
+
 @pytest.mark.parametrize("case", GOLD["cases"], ids=lambda c: f"k{c['k']}e{c['e']}L{c['len']}")
 def test_golden_batched_encode_decode(ctx, case):
     """Batched encode (specialized or generic) + device decode vs the
