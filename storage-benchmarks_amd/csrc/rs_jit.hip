@@ -486,28 +486,63 @@ __global__ __launch_bounds__(256) void k_jitw_emit(int k, int e, const uint8_t* 
     const size_t stride = (size_t)W::chunk_stride();
     uint8_t* cbase = code + ((size_t)b * 2 + w) * nch * stride;
     const int sb = W::src_bytes(nslot);
-    for (int i = threadIdx.x; i < nslot * k; i += blockDim.x)
-        cw[i] = coef[((size_t)b * e + R * w) * k + i];
+    // every load of a phase in flight before its first use: the loops below
+    // would otherwise wait a full memory latency per iteration
+    {
+        const uint8_t* cr = coef + ((size_t)b * e + R * w) * k;
+        constexpr int NB = R * 256 / 256;  // bytes per thread, nslot * k <= R * 250
+        uint8_t v[NB];
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+            const int i = threadIdx.x + 256 * j;
+            v[j] = i < nslot * k ? cr[i] : 0;
+        }
+#pragma unroll
+        for (int j = 0; j < NB; ++j)
+            cw[threadIdx.x + 256 * j] = v[j];
+    }
     __syncthreads();
     // (source, slot) runs of 64 bytes, one 16-byte quarter (planes 2j, 2j+1)
-    // per thread, so a wave's store covers 1 KB of consecutive code
-    for (int i = threadIdx.x; i < R * k * 4; i += blockDim.x) {
-        const int run = i >> 2, j = i & 3;
-        const int q = run / R, s = run - q * R;
-        if (s >= nslot)
-            continue;
-        const int ch = q / CS, t = q - ch * CS;
-        const uint4 bw = *reinterpret_cast<const uint4*>(&kWideTab.mac[8 * cw[s * k + q] + 2 * j]);
-        const int acc = W::ACC + 8 * s + 2 * j;
-        const uint64_t w0 = W::with_acc((uint64_t)bw.y << 32 | bw.x, acc);
-        const uint64_t w1 = W::with_acc((uint64_t)bw.w << 32 | bw.z, acc + 1);
-        reinterpret_cast<uint4*>(cbase + (size_t)ch * stride + (size_t)t * sb + W::PRE + 64 * s)[j] =
-            make_uint4((uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1, (uint32_t)(w1 >> 32));
+    // per thread, so a wave's store covers 1 KB of consecutive code; U table
+    // loads issued together
+    constexpr int U = 8;
+    for (int i0 = threadIdx.x; i0 < R * k * 4; i0 += 256 * U) {
+        uint4 bw[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int i = i0 + 256 * u, run = i >> 2, q = run / R, s = run - q * R;
+            const int c = i < R * k * 4 && s < nslot ? cw[s * k + q] : 0;
+            bw[u] = *reinterpret_cast<const uint4*>(&kWideTab.mac[8 * c + 2 * (i & 3)]);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int i = i0 + 256 * u, run = i >> 2, j = i & 3, q = run / R, s = run - q * R;
+            if (i >= R * k * 4 || s >= nslot)
+                continue;
+            const int ch = q / CS, t = q - ch * CS;
+            const int acc = W::ACC + 8 * s + 2 * j;
+            const uint64_t w0 = W::with_acc((uint64_t)bw[u].y << 32 | bw[u].x, acc);
+            const uint64_t w1 = W::with_acc((uint64_t)bw[u].w << 32 | bw[u].z, acc + 1);
+            reinterpret_cast<uint4*>(cbase + (size_t)ch * stride + (size_t)t * sb + W::PRE + 64 * s)[j] =
+                make_uint4((uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1, (uint32_t)(w1 >> 32));
+        }
     }
-    for (int i = threadIdx.x; i < PW * k; i += blockDim.x) {  // preambles
-        const int q = i / PW, r = i - q * PW;
-        const int ch = q / CS, t = q - ch * CS;
-        reinterpret_cast<uint64_t*>(cbase + (size_t)ch * stride + (size_t)t * sb)[r] = kWideTab.pre[PW * t + r];
+    // preambles: this thread's words of the table are fixed by its index mod 14
+    for (int i0 = threadIdx.x; i0 < PW * k; i0 += 256 * 4) {
+        uint64_t pw[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int i = i0 + 256 * u, q = i / PW, r = i - q * PW, t = q % CS;
+            pw[u] = kWideTab.pre[i < PW * k ? PW * t + r : 0];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int i = i0 + 256 * u, q = i / PW, r = i - q * PW;
+            if (i >= PW * k)
+                continue;
+            const int ch = q / CS, t = q - ch * CS;
+            reinterpret_cast<uint64_t*>(cbase + (size_t)ch * stride + (size_t)t * sb)[r] = pw[u];
+        }
     }
     for (int ch = threadIdx.x; ch < nch; ch += blockDim.x) {  // returns
         const int nt = min(CS, k - CS * ch);
