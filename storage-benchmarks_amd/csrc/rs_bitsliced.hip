@@ -141,7 +141,46 @@ struct Args {
     const uint8_t* src;   // [B][K] rows
     uint8_t* out;         // [B][E] rows
     long long pitch, len;
+    long long blocks;     // B
+    int flat;             // tiles over the blocks' rows laid end to end (short rows)
 };
+
+// Where lane `lane` of column tile `tile` works: the tile's first block b0,
+// the lane's block b0 + db and byte offset o in its rows, and whether it has
+// bytes at all.  Per block, tiles cover [0, len) in 2 KB steps, the last one
+// partial (C4: 32000 = 15 x 2048 + 1280, 2.4 % of the tiles' lanes idle).
+// flat: tiles cover the B blocks' rows as one run of B x len bytes per row
+// index (len % 32 == 0, so a lane's 32 bytes never straddle two blocks) and
+// a tile's lanes may belong to consecutive blocks: one idle tail per launch.
+struct TilePos {
+    long long b0, o;
+    int db;
+    bool inb;
+};
+__device__ __forceinline__ TilePos tile_pos(const Args& a, int lane)
+{
+    TilePos p;
+    if (!a.flat) {
+        p.b0 = blockIdx.y;
+        p.o = (long long)blockIdx.x * 2048 + lane * 32;
+        p.db = 0;
+        p.inb = p.o + 32 <= a.len;
+        return p;
+    }
+    const long long t0 = (long long)blockIdx.x * 2048;
+    p.b0 = t0 / a.len;                                // wave-uniform
+    const int x = (int)(t0 - p.b0 * a.len) + lane * 32;  // < len + 2048 < 2^24
+    int db = (int)((float)x * (1.0f / (float)a.len));
+    const int L = (int)a.len;
+    if (x - db * L >= L)
+        ++db;
+    if (x - db * L < 0)
+        --db;
+    p.db = db;
+    p.o = x - (long long)db * L;
+    p.inb = p.b0 + db < a.blocks;
+    return p;
+}
 
 // LDS part: S sources of [2 halves][64 lanes] x 16 B; two parts double-buffer
 // the source stream (2 x 16 KiB).  A plan chunk of C sources is ceil(C/S)
@@ -194,11 +233,12 @@ __device__ __forceinline__ void run_group(const Args& a, uint4 (*lds)[S * 2 * 64
     static_assert(NR > 0, "empty wave group");
 
     const int lane = threadIdx.x & 63;
-    const int b = blockIdx.y;
-    const long long off = (long long)blockIdx.x * 2048 + lane * 32;
-    const bool inb = off + 32 <= a.len;
-    const long long loff = inb ? off : 0;  // out-of-range lanes re-read the row head
-    const uint8_t* sb = a.src + (size_t)b * K * a.pitch;
+    const TilePos tp = tile_pos(a, lane);
+    const bool inb = tp.inb;
+    // source offset from the tile's first block; out-of-range lanes re-read
+    // the row head
+    const long long loff = inb ? tp.db * (long long)K * a.pitch + tp.o : 0;
+    const uint8_t* sb = a.src + (size_t)tp.b0 * K * a.pitch;
     auto live = [&](int j) { return j < K; };
     const uint32_t m4 = vconst(0x0F0F0F0Fu), m2 = vconst(0x33333333u), m1 = vconst(0x55555555u);
     const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint4*)&lds[0][0];
@@ -269,7 +309,8 @@ __device__ __forceinline__ void run_group(const Args& a, uint4 (*lds)[S * 2 * 64
 
     if (!inb)
         return;
-    uint8_t* ob = a.out + (size_t)b * E * a.pitch;
+    uint8_t* ob = a.out + (size_t)tp.b0 * E * a.pitch;
+    const long long ooff = tp.db * (long long)E * a.pitch + tp.o;
 #pragma unroll
     for (int r = 0; r < NR; ++r) {
         uint32_t W[8];
@@ -277,7 +318,7 @@ __device__ __forceinline__ void run_group(const Args& a, uint4 (*lds)[S * 2 * 64
         for (int q = 0; q < 8; ++q)
             W[q] = acc[r][q];
         tr8(W, m4, m2, m1);
-        store32(ob + (size_t)(R0 + r) * a.pitch, off, W);
+        store32(ob + (size_t)(R0 + r) * a.pitch, ooff, W);
     }
 }
 
@@ -375,7 +416,7 @@ template <int K, int E>
 hipError_t launch_split(const uint8_t* src, uint8_t* out, long long pitch, long long len, long long blocks,
                         hipStream_t st)
 {
-    Args a{src, out, pitch, len};
+    Args a{src, out, pitch, len, blocks, 0};
     dim3 grid((unsigned)((len + 2047) / 2048), (unsigned)blocks);
     hipLaunchKernelGGL((k_rs_bs_split<K, E, 4>), grid, dim3(256), 0, st, a);
     return hipGetLastError();
@@ -385,8 +426,12 @@ template <int K, int E, int C, int NW>
 hipError_t launch(const uint8_t* src, uint8_t* out, long long pitch, long long len,
                   long long blocks, hipStream_t st)
 {
-    Args a{src, out, pitch, len};
-    dim3 grid((unsigned)((len + 2047) / 2048), (unsigned)blocks);
+    // short rows whose last tile is partial: tiles over the rows of all
+    // blocks end to end (tile_pos)
+    const bool flat = blocks > 1 && len % 2048 != 0 && len < 65536 && pitch % 32 == 0;
+    Args a{src, out, pitch, len, blocks, flat ? 1 : 0};
+    dim3 grid(flat ? (unsigned)((blocks * len + 2047) / 2048) : (unsigned)((len + 2047) / 2048),
+              flat ? 1u : (unsigned)blocks);
     hipLaunchKernelGGL((k_rs_bs<K, E, C, NW>), grid, dim3(64 * NW), 0, st, a);
     return hipGetLastError();
 }

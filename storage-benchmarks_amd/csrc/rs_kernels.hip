@@ -911,21 +911,26 @@ __global__ __launch_bounds__(256) void k_decode_prepare_syn(int k, int e,
     const int b = blockIdx.x;
     const int tid = threadIdx.x, nt = blockDim.x;
     const uint8_t* eb = err + (size_t)b * e;
+    uint8_t* lv = A + e * e;   // survivors, k - e bytes (256 reserved)
+    uint8_t* lam = lv + 256;   // Lambda coefficients, e + 1 (64 reserved)
+    uint8_t* lw = lam + 64;    // log w_i (64 reserved)
+    uint8_t* lb = lw + 64;     // log Lambda(b_q) (256 reserved)
+    uint8_t* ea = lb + 256;    // the erased originals j_i (64 reserved)
+    uint8_t* aa = ea + 64;     // a_i = 2^(j_i) (64 reserved)
     for (int i = tid; i < 512; i += nt) {
         gexp[i] = kGfTables.exp[i];
         if (i < 256)
             glog[i] = kGfTables.log[i];
     }
-    if (tid == 0) {
-        // validate: strictly ascending originals
-        int bad = 0;
-        for (int i = 0; i < e; ++i) {
-            const int j = eb[i];
-            if (j >= k || (i > 0 && j <= eb[i - 1]))
-                bad = 1;
-        }
-        sh[0] = bad ? -2 : 0;
-    }
+    if (tid < e)  // the list once from global memory, all lanes at once
+        ea[tid] = eb[tid];
+    if (tid == 0)
+        sh[0] = 0;
+    __syncthreads();
+    // validate: strictly ascending originals (one lane per entry; a serial
+    // loop of dependent byte loads here was most of this kernel's time)
+    if (tid < e && (ea[tid] >= k || (tid > 0 && ea[tid] <= ea[tid - 1])))
+        sh[0] = -2;
     __syncthreads();
     if (sh[0] != 0) {
         if (tid == 0)
@@ -949,17 +954,9 @@ __global__ __launch_bounds__(256) void k_decode_prepare_syn(int k, int e,
         //   (V_E^-1)[i][p]          = [z^p] L_i(z) = [z^p] (Lambda(z) / (z + a_i)) / w_i
         //   (V_E^-1 V_kept)[i][q]   = L_i(b_q)     = Lambda(b_q) / ((b_q + a_i) w_i)
         // with b_q = 2^(j_q) for survivor q: O(e k) work, no elimination.
-        uint8_t* lv = A + e * e;   // survivors, k - e bytes (256 reserved)
-        uint8_t* lam = lv + 256;   // Lambda coefficients, e + 1 (64 reserved)
-        uint8_t* lw = lam + 64;    // log w_i (64 reserved)
-        uint8_t* lb = lw + 64;     // log Lambda(b_q) (256 reserved)
-        uint8_t* ea = lb + 256;    // the erased originals j_i (64 reserved)
-        uint8_t* aa = ea + 64;     // a_i = 2^(j_i) (64 reserved)
         const int nl = k - e;
-        for (int i = tid; i < e; i += nt) {  // the list once from global memory
-            ea[i] = eb[i];
-            aa[i] = gexp[eb[i]];
-        }
+        for (int i = tid; i < e; i += nt)
+            aa[i] = gexp[ea[i]];
         __syncthreads();
         for (int j = tid; j < k; j += nt) {
             int below = 0;  // erased originals < j (the list is validated ascending)

@@ -102,3 +102,26 @@ def test_compiled_equals_generated_at_size(ctx):
     ctx.set_encode_kernel("auto")
     torch.cuda.synchronize()
     assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("k,e", [(64, 32), (16, 4), (100, 20), (64, 16)])
+@pytest.mark.parametrize("L,B", [(32, 67), (96, 5), (1056, 3), (2080, 2), (32000, 3), (63488 + 32, 2)])
+def test_compiled_encode_short_rows_flat(ctx, orc, k, e, L, B):
+    """Short rows with a partial last tile run the compiled encode with the
+    tiles laid over all blocks' rows end to end (rs_bitsliced.hip tile_pos:
+    one tile's lanes may belong to consecutive blocks, up to 64 of them at
+    L = 32): every block's parity equals the oracle's and the row padding
+    beyond L is left as it was."""
+    ctx.set_encode_kernel("compiled")
+    try:
+        encode_and_check(ctx, orc, k, e, L, B)
+        dev = torch.device("cuda", 0)
+        pitch = (L + 255) // 256 * 256
+        src = torch.empty(B * k * pitch, dtype=torch.uint8, device=dev)
+        par = torch.full((B * e * pitch,), 0x5A, dtype=torch.uint8, device=dev)
+        ctx.fill_synthetic(src, B * k, L, pitch, 3, 0)
+        ctx.encode_blocks(k, e, L, pitch, B, src, par)
+        torch.cuda.synchronize()
+        assert (par.view(B, e, pitch)[:, :, L:] == 0x5A).all()
+    finally:
+        ctx.set_encode_kernel("auto")

@@ -1,4 +1,5 @@
 # streamed C4: decode prepare beside the encode (default) vs after it, two
+# (the --serial-prepare A/B of the round-3 overlap experiment; bench.py no longer has the overlap)
 # passes; the C4 GPU tests: bash tools/r03_c4ovl.sh TAG
 set -o pipefail
 O=gpurun_out/r03_$1; mkdir -p $O
