@@ -18,7 +18,7 @@ inline int value_reg(int v, int bank) { return v < 8 ? plane_reg(bank, v) : 32 +
 
 // The full four-Russians tables (L[n] over planes 0-3, H[n] over 4-7, the 22
 // composites of rs_jit.h's fixed layout) as a program: always a cover.
-void full_tables(const uint8_t (&masks)[64], int nm, SrcProg& p)
+void full_tables(const uint8_t (&masks)[8 * kMaxSlots], int nm, SrcProg& p)
 {
     uint8_t id[256];
     memset(id, kNone, sizeof id);
@@ -48,7 +48,7 @@ void full_tables(const uint8_t (&masks)[64], int nm, SrcProg& p)
 
 void plan_source(const uint8_t* coef, int nslot, SrcProg& p, int max_ops)
 {
-    uint8_t masks[64];
+    uint8_t masks[8 * kMaxSlots];
     const int nm = 8 * nslot;
     for (int s = 0; s < nslot; ++s)
         for (int b = 0; b < 8; ++b)
@@ -80,7 +80,7 @@ void plan_source(const uint8_t* coef, int nslot, SrcProg& p, int max_ops)
     bool over = false;
     for (;;) {
         int nneed = 0;
-        uint8_t nl[64];
+        uint8_t nl[256];
         for (int m = 1; m < 256; ++m)
             if (need[m])
                 nl[nneed++] = (uint8_t)m;
@@ -244,6 +244,93 @@ std::vector<uint8_t> build_matrix_code(const uint8_t* c, int k, int e, int* chun
                 emit_chunk(&code[(((size_t)p * 4 + w) * nch + ch) * stride], nt, nslot, progs);
             }
         }
+    }
+    return code;
+}
+
+namespace {
+
+// value id -> VGPR in the two-wave layout (rs_jit.h Wide)
+inline int wide_reg(int v) { return v < 8 ? 10 + v : 18 + (v - 8); }
+
+// One chunk of the two-wave layout at dst (nullptr: size only).
+size_t emit_chunk_wide(uint8_t* dst, int nt, int nslot, const SrcProg* progs)
+{
+    size_t o = 0;
+    auto put32 = [&](uint32_t w) {
+        if (dst)
+            memcpy(dst + o, &w, 4);
+        o += 4;
+    };
+    auto put64 = [&](uint64_t w) {
+        if (dst)
+            memcpy(dst + o, &w, 8);
+        o += 8;
+    };
+    for (int t = 0; t < nt; ++t) {
+        put64(enc_ds_read_b128(10, 9, t * LDS_SRC));
+        put64(enc_ds_read_b128(14, 9, t * LDS_SRC + LDS_HALF));
+        put32(enc_waitcnt_lgkm(0));
+        const SrcProg& p = progs[t];
+        for (int i = 0; i < p.nops; ++i) {
+            const int d = 18 + i, a = wide_reg(p.ops[i][0]), b = wide_reg(p.ops[i][1]);
+            if (p.ops[i][2] == kNone)
+                put32(enc_xor_e32(d, a, b));
+            else
+                put64(enc_bitop3_96(d, a, b, wide_reg(p.ops[i][2])));
+        }
+        for (int s = 0; s < nslot; ++s)
+            for (int b = 0; b < 8; ++b) {
+                const uint8_t* q = p.outs[8 * s + b];
+                const int acc = 40 + 8 * s + b;
+                if (q[0] == kNone)
+                    continue;  // zero mask: nothing to add
+                if (q[1] == kNone)
+                    put64(enc_xor_e64(acc, acc, wide_reg(q[0])));
+                else
+                    put64(enc_bitop3_96(acc, acc, wide_reg(q[0]), wide_reg(q[1])));
+            }
+    }
+    put64((uint64_t)S_NOP0 << 32 | S_SETPC_82);
+    return o;
+}
+
+}  // namespace
+
+std::vector<uint8_t> build_matrix_code_wide(const uint8_t* c, int k, int e, int R, int CS, int* chunk_stride,
+                                            int max_ops)
+{
+    const int nch = (k + CS - 1) / CS;
+    // programs of every (wave, source), then the chunk sizes
+    std::vector<SrcProg> progs((size_t)2 * k);
+    for (int w = 0; w < 2; ++w) {
+        const int nslot = std::min(R, e - R * w);
+        for (int q = 0; q < k && nslot > 0; ++q) {
+            uint8_t cf[kMaxSlots];
+            for (int s = 0; s < nslot; ++s)
+                cf[s] = c[(size_t)(R * w + s) * k + q];
+            plan_source(cf, nslot, progs[(size_t)w * k + q], max_ops);
+        }
+    }
+    size_t most = 0;
+    for (int w = 0; w < 2; ++w) {
+        const int nslot = std::min(R, e - R * w);
+        for (int ch = 0; ch < nch && nslot > 0; ++ch)
+            most = std::max(most, emit_chunk_wide(nullptr, std::min(CS, k - CS * ch), nslot,
+                                                  &progs[(size_t)w * k + CS * ch]));
+    }
+    const int stride = (int)((most + 63) / 64 * 64);
+    *chunk_stride = stride;
+    std::vector<uint8_t> code((size_t)2 * nch * stride);
+    for (size_t i = 0; i + 8 <= code.size(); i += 8) {
+        const uint64_t ret = (uint64_t)S_NOP0 << 32 | S_SETPC_82;
+        memcpy(&code[i], &ret, 8);
+    }
+    for (int w = 0; w < 2; ++w) {
+        const int nslot = std::min(R, e - R * w);
+        for (int ch = 0; ch < nch && nslot > 0; ++ch)
+            emit_chunk_wide(&code[((size_t)w * nch + ch) * stride], std::min(CS, k - CS * ch), nslot,
+                            &progs[(size_t)w * k + CS * ch]);
     }
     return code;
 }

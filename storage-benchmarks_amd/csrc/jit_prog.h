@@ -24,6 +24,8 @@ namespace jit {
 constexpr int kMaxComposites = 22;  // v32..v53
 constexpr uint8_t kNone = 255;
 
+constexpr int kMaxSlots = 16;       // rows per wave: 8 (k_rs_jit), up to 16 (k_rs_jitw)
+
 // One (wave, source) program: value ids 0..7 are the source's planes
 // (bit i of a mask = plane i), 8 + i the composite ops[i] = XOR of its 2 or 3
 // operand values; accumulator plane b of slot s gets outs[8 s + b] (0, 1 or
@@ -31,11 +33,11 @@ constexpr uint8_t kNone = 255;
 struct SrcProg {
     int nops = 0;
     uint8_t ops[kMaxComposites][3];
-    uint8_t outs[64][2];
+    uint8_t outs[8 * kMaxSlots][2];
 };
 
 // Cover of the masks of coefficients coef[0..nslot-1] (slot s = output row
-// 8 w + s of the wave).
+// R w + s of the wave), nslot <= kMaxSlots.
 void plan_source(const uint8_t* coef, int nslot, SrcProg& p, int max_ops = kMaxComposites);
 
 // Largest chunk (8 sources, 8 slots, kMaxComposites 3-input composites),
@@ -53,6 +55,16 @@ size_t emit_chunk(uint8_t* dst, int nt, int nslot, const SrcProg* progs);
 // the full-table fallback).
 std::vector<uint8_t> build_matrix_code(const uint8_t* c, int k, int e, int* chunk_stride,
                                        int max_ops = kMaxComposites);
+
+// The same in the two-wave layout of k_rs_jitw (rs_jit.h Wide<R, CS>, the
+// register contract of the decode: planes v10..v17, composites v18..v39,
+// accumulators from v40, LDS address in v9) for 16 < e <= 32: wave w (rows
+// R w .. R w + R - 1), chunk ch of CS sources at (w nch + ch) stride, each
+// source loading its own planes, then its covered composites and one
+// instruction per nonzero output mask.  *chunk_stride = the largest chunk
+// rounded to 64 bytes.
+std::vector<uint8_t> build_matrix_code_wide(const uint8_t* c, int k, int e, int R, int CS, int* chunk_stride,
+                                            int max_ops = kMaxComposites);
 
 }  // namespace jit
 }  // namespace rsgpu

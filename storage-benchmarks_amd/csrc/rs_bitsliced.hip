@@ -445,6 +445,15 @@ bool rs_bitsliced_available(int k, int e)
            (k == 64 && e == 16);
 }
 
+int rs_bitsliced_rows_per_wave(int k, int e)
+{
+    // (E + NW - 1) / NW of launch_rs_bitsliced's plans
+    if (!rs_bitsliced_available(k, e))
+        return 0;
+    const int nw = (k == 64 && e == 32) || (k == 100 && e == 20) ? 4 : (k == 64 && e == 16) ? 2 : 1;
+    return (e + nw - 1) / nw;
+}
+
 bool rs_bitsliced_split_available(int k, int e)
 {
     return (k == 16 && e == 4) || (k == 16 && e == 8) || (k == 5 && e == 4) || (k == 20 && e == 7);

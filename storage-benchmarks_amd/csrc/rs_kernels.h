@@ -65,6 +65,9 @@ hipError_t launch_compare_rows(const uint8_t* src, long long src_pitch, int k, c
 // coefficients (rs_bitsliced.hip).  Requires len % 32 == 0, 16-byte aligned
 // rows.
 bool rs_bitsliced_available(int k, int e);
+// output rows each wave of the compiled kernel owns (its composites of a
+// source are built per this many rows), 0 if none is compiled for (k, e)
+int rs_bitsliced_rows_per_wave(int k, int e);
 hipError_t launch_rs_bitsliced(int k, int e, const uint8_t* src, uint8_t* out, long long pitch,
                                long long len, long long blocks, hipStream_t st);
 // Small batches of the single-chunk codes (16,4) (16,8) (5,4) (20,7): four

@@ -262,18 +262,49 @@ int jit_ensure(rsgpu_ctx* ctx, size_t bytes)
 // block (jit_prog.h) in ctx->d_enc_code; rebuilt only when the matrix
 // changes.  Stream-ordered: the copy into the executable buffer runs after
 // every kernel enqueued before it, which may still run the old program.
+// One block's code in the two-wave layout (rs_jit.h Wide<R, CS>) for the
+// e x k matrix coef, from Wide::code_word: wave w, chunk ch at
+// (w nch + ch) chunk_stride; unused words are returns.
+template <class W>
+void jitw_emit_host(int k, int e, const unsigned char* coef, uint64_t* o64)
+{
+    const int nch = (k + W::CS - 1) / W::CS, stride_w = W::chunk_stride() / 8;
+    for (int w = 0; w < 2; ++w) {
+        const int nslot = std::min(W::R, e - W::R * w);
+        const unsigned char* rows = coef + (size_t)W::R * w * k;
+        for (int ch = 0; ch < nch; ++ch)
+            for (int o = 0; o < stride_w; ++o) {
+                uint64_t word;
+                if (W::code_word(rows, k, nslot, ch, o, &word))
+                    o64[((size_t)w * nch + ch) * stride_w + o] = word;
+            }
+    }
+}
+
+int jitw_cs(int e) { return jitw_rows(e) == 16 ? jit::J16::CS : jitw_rows(e) == 12 ? jit::J12::CS : jit::J10::CS; }
+
+// The shared program of a matrix (jit_prog.h, composites by greedy cover):
+// for 16 < rows <= 32 in the two-wave layout of the decode (k_rs_jitw: a
+// source's composites built twice per tile), else the 8-row layout (k_rs_jit).
 int shared_program(rsgpu_ctx* ctx, const uint8_t* coef, int k, int rows)
 {
-    std::vector<uint8_t> key(8 + (size_t)k * rows);
+    const bool wide = jitw_rows(rows) != 0;
+    std::vector<uint8_t> key(9 + (size_t)k * rows);
     std::memcpy(key.data(), &k, 4);
     std::memcpy(key.data() + 4, &rows, 4);
-    std::memcpy(key.data() + 8, coef, (size_t)k * rows);
+    key[8] = wide ? 1 : 0;
+    std::memcpy(key.data() + 9, coef, (size_t)k * rows);
     if (ctx->d_enc_code && key == ctx->enc_key)
         return RSGPU_OK;
     if (jit_probe(ctx) != 1)
         return fail(ctx, RSGPU_ERR_UNSUPPORTED, "no executable device memory pool");
     int stride = 0;
-    const std::vector<uint8_t> code = jit::build_matrix_code(coef, k, rows, &stride);
+    std::vector<uint8_t> code;
+    if (wide) {
+        code = jit::build_matrix_code_wide(coef, k, rows, jitw_rows(rows), jitw_cs(rows), &stride);
+    } else {
+        code = jit::build_matrix_code(coef, k, rows, &stride);
+    }
     if (ctx->enc_code_bytes < code.size()) {
         RS_HIP(ctx, hipStreamSynchronize(ctx->stream));
         if (ctx->d_enc_code)
@@ -318,6 +349,23 @@ int shared_program_launch(rsgpu_ctx* ctx, const uint8_t* coef, int k, int rows, 
     int rc = shared_program(ctx, coef, k, rows);
     if (rc)
         return rc;
+    if (jitw_rows(rows)) {  // one launch of the two-wave kernel, every block on the same code
+        JitArgs j{};
+        j.srcs = d_srcs;
+        j.dsts = d_dsts;
+        j.code = (const uint8_t*)ctx->d_enc_code;
+        j.chunk_stride = ctx->enc_chunk_stride;
+        j.block_stride = 0;
+        j.k = k;
+        j.rows = rows;
+        j.dst_stride = rows;
+        j.len = len;
+        j.status = nullptr;
+        j.tiles_per_wg = 2;
+        KTimer kt(ctx, name, (size_t)blocks);
+        RS_HIP(ctx, launch_rs_jitw(j, blocks, ctx->stream));
+        return RSGPU_OK;
+    }
     const int nch = (k + 7) / 8;
     for (int p = 0; p * 32 < rows; ++p) {
         JitArgs j{};
@@ -876,7 +924,14 @@ int rsgpu_encode_blocks(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch, 
                                               (long long)blocks, ctx->stream));
         return RSGPU_OK;
     }
-    if (compiled_ok && !coef && aligned && len % 32 == 0 && rs_bitsliced_available(k, e)) {
+    // AUTO leaves the compiled kernel when its waves own fewer than 8 rows and
+    // the two-wave generated layout covers e (16 < e <= 32): (100, 20) builds
+    // every source's composites per 5 rows there, per 10 rows in k_rs_jitw --
+    // C5 encode 12.8-13.0 vs 14.4 ms (profiles/r03_ab/wide_encode/)
+    const bool compiled_pays = ctx->encode_kernel == RSGPU_ENCODE_COMPILED ||
+                               rs_bitsliced_rows_per_wave(k, e) >= 8 || !jitw_rows(e) ||
+                               !(len % 32 == 0 && jit_probe(ctx) == 1);
+    if (compiled_ok && compiled_pays && !coef && aligned && len % 32 == 0 && rs_bitsliced_available(k, e)) {
         KTimer kt(ctx, "k_rs_bs(encode)", blocks);
         RS_HIP(ctx, launch_rs_bitsliced(k, e, d_src, d_parity, (long long)pitch, (long long)len,
                                         (long long)blocks, ctx->stream));
@@ -1523,22 +1578,6 @@ long long rsgpu_internal_jit_emit(int k, int e, const unsigned char* coef, unsig
 // Test hook (not part of include/rsgpu.h): the same for the two-wave layouts
 // of k_rs_jitw (rs_jit.h Wide, R = 16 for 24 < e <= 32, 10 for 16 < e <= 20),
 // from Wide::code_word (the words k_jitw_emit writes).
-extern "C++" template <class W>
-static void jitw_emit_host(int k, int e, const unsigned char* coef, uint64_t* o64)
-{
-    const int nch = (k + W::CS - 1) / W::CS, stride_w = W::chunk_stride() / 8;
-    for (int w = 0; w < 2; ++w) {
-        const int nslot = std::min(W::R, e - W::R * w);
-        const unsigned char* rows = coef + (size_t)W::R * w * k;
-        for (int ch = 0; ch < nch; ++ch)
-            for (int o = 0; o < stride_w; ++o) {
-                uint64_t word;
-                if (W::code_word(rows, k, nslot, ch, o, &word))
-                    o64[((size_t)w * nch + ch) * stride_w + o] = word;
-            }
-    }
-}
-
 long long rsgpu_internal_jitw_emit(int k, int e, const unsigned char* coef, unsigned char* out,
                                    size_t out_bytes)
 {
@@ -1557,6 +1596,22 @@ long long rsgpu_internal_jitw_emit(int k, int e, const unsigned char* coef, unsi
     else
         jitw_emit_host<jit::J10>(k, e, coef, o64);
     return (long long)need;
+}
+
+// Test hook (not in include/rsgpu.h): the host-built shared program of an
+// e x k matrix in the two-wave layout (16 < e <= 32), for the CPU suite to
+// disassemble and interpret.  Returns the bytes needed, or -1; writes only
+// when out_bytes is large enough; *chunk_stride gets the stride.
+long long rsgpu_internal_jitw_matrix_code(int k, int e, const unsigned char* coef, unsigned char* out,
+                                          size_t out_bytes, int* chunk_stride, int max_ops)
+{
+    if (k <= 0 || k + e > 250 || !jitw_rows(e) || !coef || !chunk_stride)
+        return -1;
+    const std::vector<uint8_t> code =
+        jit::build_matrix_code_wide(coef, k, e, jitw_rows(e), jitw_cs(e), chunk_stride, max_ops);
+    if (out && out_bytes >= code.size())
+        std::memcpy(out, code.data(), code.size());
+    return (long long)code.size();
 }
 
 // Test hook (not part of include/rsgpu.h): the DEVICE emitter k_jitw_emit

@@ -240,6 +240,80 @@ def test_shared_matrix_code(k, e, kind):
         assert n_comp / n_src < 18, n_comp / n_src
 
 
+def matrix_code_wide(k, e, coef, max_ops=22):
+    import rsgpu
+    f = rsgpu.lib().rsgpu_internal_jitw_matrix_code
+    f.restype = C.c_longlong
+    f.argtypes = [C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_size_t, C.POINTER(C.c_int), C.c_int]
+    coef = np.ascontiguousarray(coef, np.uint8)
+    stride = C.c_int()
+    need = f(k, e, coef.ctypes.data, None, 0, C.byref(stride), max_ops)
+    out = np.zeros(need, np.uint8)
+    assert f(k, e, coef.ctypes.data, out.ctypes.data, need, C.byref(stride), max_ops) == need
+    return out.tobytes(), stride.value
+
+
+@pytest.mark.parametrize("k,e,kind", [(64, 32, "rs"), (100, 20, "rs"), (100, 25, "random"),
+                                      (128, 32, "random"), (48, 24, "random"), (17, 17, "random"),
+                                      (24, 17, "capped"), (218, 32, "rs")])
+def test_shared_matrix_code_wide(k, e, kind):
+    """The GENERATED encode's host-built code for 16 < e <= 32 in the
+    decode's two-wave layout (jit_prog.cpp build_matrix_code_wide: planes
+    v10..v17 from LDS at v9, covered composites from v18, accumulators from
+    v40): interpreted chunk by chunk, every accumulator equals sum_q c[row][q]
+    * src_q over GF(2^8), registers stay in v9..v(40+8R-1), every register is
+    read after its LDS load was waited for, and the covers average under the
+    22 composites of the full tables."""
+    R = 16 if e > 24 else 12 if e > 20 else 10
+    cs = WIDE[R][0]
+    rng = random.Random(k * 1000 + e)
+    if kind == "rs":
+        coef = rs_rows(k, e)
+    else:
+        coef = np.array([[rng.randrange(256) for _ in range(k)] for _ in range(e)], np.uint8)
+        coef[0, 0] = 0
+    code, stride = matrix_code_wide(k, e, coef, 6 if kind == "capped" else 22)
+    nch = (k + cs - 1) // cs
+    assert stride % 64 == 0 and len(code) == 2 * nch * stride
+    src = [[rng.randrange(256) for _ in range(32)] for _ in range(k)]
+    n_comp = n_src = 0
+    for w in range(2):
+        nslot = min(R, e - R * w)
+        regs = {r: 0 for r in range(256)}
+        pending = []
+        for ch in range(nch):
+            base = (w * nch + ch) * stride
+            nt = min(cs, k - cs * ch)
+            ins = disasm(code[base:base + stride])
+            end = next(off for off, m, _ in ins if m == "s_setpc_b64")
+            ins = [x for x in ins if x[0] <= end]
+            n_comp += sum(1 for off, m, ops in ins if m in ("v_xor_b32_e32", "v_bitop3_b32")
+                          and int(regs_of(ops.split(",")[0])[0]) < 40)
+            n_src += nt
+            used = [int(n) for _, _, ops in ins for n in re.findall(r"v\[?(\d+)", ops)]
+            used += [int(n) for _, _, ops in ins for n in re.findall(r"v\[\d+:(\d+)\]", ops)]
+            assert max(used) < 40 + 8 * R and min(used) >= 9
+            lds = {}
+            for t in range(nt):
+                pl = planes(src[cs * ch + t])
+                for a in range(8):
+                    lds[t * 2048 + (a // 4) * 1024 + 4 * (a % 4)] = pl[a]
+            run_chunk(ins, regs, lds, pending, addr_reg="v9")
+            assert not pending, "a load left outstanding at the return"
+        for s in range(nslot):
+            row = R * w + s
+            want = [0] * 32
+            for q in range(k):
+                want = [x ^ g.gf_mul(int(coef[row, q]), y) for x, y in zip(want, src[q])]
+            got = unplanes([regs[40 + 8 * s + b] for b in range(8)])
+            assert got == want, (k, e, row)
+    # per (wave, source): the capped covers fall back to the full tables
+    if kind == "capped":
+        assert n_comp / n_src > 18, n_comp / n_src
+    else:
+        assert n_comp / n_src < 20, n_comp / n_src
+
+
 def emitw(k, e, coef):
     import rsgpu
     f = rsgpu.lib().rsgpu_internal_jitw_emit
