@@ -125,3 +125,20 @@ def test_compiled_encode_short_rows_flat(ctx, orc, k, e, L, B):
         assert (par.view(B, e, pitch)[:, :, L:] == 0x5A).all()
     finally:
         ctx.set_encode_kernel("auto")
+
+
+@pytest.mark.parametrize("k,e,name", [(100, 20, "k_rs_jit(encode)"), (64, 32, "k_rs_bs(encode)"),
+                                      (64, 16, "k_rs_bs(encode)")])
+def test_auto_encode_kernel_choice(ctx, orc, k, e, name):
+    """AUTO keeps a compiled kernel whose waves own >= 8 rows and takes the
+    two-wave generated program (composites per 10 rows) over (100, 20)'s
+    compiled kernel (composites per 5 rows); parity equals the oracle's."""
+    ctx.set_encode_kernel("auto")
+    ctx.timing_read()
+    ctx.timing_enable(True)
+    try:
+        encode_and_check(ctx, orc, k, e, 8192, 3)
+        names = [n for n, _, _ in ctx.timing_read()]
+    finally:
+        ctx.timing_enable(False)
+    assert names and names[-1] == name, names
