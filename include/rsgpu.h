@@ -125,13 +125,17 @@ int rsgpu_encode_blocks(rsgpu_ctx *ctx, int k, int e, size_t len, size_t pitch, 
 /* Encode kernel of rsgpu_encode_blocks / rsgpu_ec_encode_data (per context;
  * every choice writes the same bytes):
  *   AUTO       COMPILED for the codes built in (gf_gen_rs_matrix (k, e) in
- *              {(16,4) (16,8) (64,32) (64,16) (100,20) (5,4) (20,7)}, no
- *              `coef`), otherwise GENERATED (aligned rows, len % 32 == 0),
+ *              {(16,4) (16,8) (64,32) (64,16) (5,4) (20,7)}, no `coef`),
+ *              otherwise GENERATED (aligned rows, len % 32 == 0; (100,20),
+ *              compiled too, runs GENERATED: its compiled waves own 5 rows),
  *              otherwise the v_perm kernel
- *   COMPILED   k_rs_bs: the matrix compiled into the kernel (codes above)
- *   GENERATED  k_rs_jit with code built on the host for the matrix, once,
- *              shared by every block: per source only the composites its
- *              coefficients need (greedy cover); rows in passes of 32
+ *   COMPILED   k_rs_bs: the matrix compiled into the kernel (codes above
+ *              and (100,20))
+ *   GENERATED  code built on the host for the matrix, once, shared by every
+ *              block: per (wave, source) only the composites its
+ *              coefficients need (greedy cover); 2 waves x 16 / 12 / 10 rows
+ *              for 16 < e <= 32 (k_rs_jitw, the decode's layout), else
+ *              waves of 8 rows in passes of 32 (k_rs_jit)
  *   THREADED   k_rs_tc: 256 generated handlers, one dispatch per coefficient
  * A choice that does not apply falls back in that order. */
 #define RSGPU_ENCODE_AUTO 0
