@@ -381,6 +381,29 @@ def test_bench_spawns_its_own_ranks():
         assert r["err_sha"] == hashlib.sha256(err.tobytes()).hexdigest()
 
 
+def test_bench_under_torch_distributed_run():
+    """The driver's scaling launch: `python -m torch.distributed.run
+    --nproc-per-node 2 ... bench.py --gpus 2` (ranks from WORLD_SIZE/RANK in
+    the environment, no self-spawn), here both ranks on device 0 over gloo."""
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.join(ROOT, "bench.py"), "--gpus", "2", "--same-device", "--dist-backend", "gloo",
+           "--config", "c3", "--blocks", "4", "--steps", "2", "--warmup", "1", "--no-cpu-baseline"]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["verified"]
+    ranks = sorted(line["ranks"], key=lambda q: q["rank"])
+    assert [(q["block0"], q["blocks"]) for q in ranks] == [(0, 4), (4, 4)]
+
+
 def test_bench_rejects_world_mismatch():
     env = dict(os.environ, WORLD_SIZE="1", RANK="0")
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"],
