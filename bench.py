@@ -395,7 +395,11 @@ def launch_cost(torch, n=400):
             "empty_kernel_us_host": round(host * 1e6 / n, 3)}
 
 
-def kernel_stats(recs, steps, alg):
+def kernel_stats(recs, steps, alg, blocks_step):
+    """Per kernel: launches, durations and the algorithmic rate.  A kernel
+    that covers a block's rows in passes (e > 32: one launch per 32 rows)
+    sees each block once per pass; its algorithmic bytes ((k + e) L per
+    block) count once per step, so a launch carries 1 / passes of them."""
     per, each = {}, {}
     for name, ms, nb in recs:
         d = per.setdefault(name, [0.0, 0, 0])
@@ -405,10 +409,13 @@ def kernel_stats(recs, steps, alg):
         each.setdefault(name, []).append(ms)
     kernels = {}
     for name, (tot, n, nb) in per.items():
+        passes = max(1, round(nb / (blocks_step * steps)))
+        per[name].append(passes)
         kernels[name] = {"avg_ms": round(tot / n, 3), "median_ms": round(statistics.median(each[name]), 3),
                          "launches": n,
                          "blocks_per_launch": nb / n,
-                         "alg_GBps": round(alg.get(name, 0.0) * nb / (tot * 1e-3) / 1e9, 1),
+                         "passes": passes,
+                         "alg_GBps": round(alg.get(name, 0.0) * nb / passes / (tot * 1e-3) / 1e9, 1),
                          "ms_per_step": round(tot / steps, 3)}
     return per, kernels
 
@@ -504,6 +511,7 @@ def alg_bytes(k, e, L):
             "k_dot_generic(decode)": blk_op,
             "k_rs_tc(encode)": blk_op, "k_rs_tc(decode)": blk_op, "k_rs_jit(decode)": blk_op,
             "k_rs_jit16(decode)": blk_op, "k_rs_jit10(decode)": blk_op, "k_rs_jit12(decode)": blk_op, "k_rs_jit(encode)": blk_op,
+            "k_rs_jit16x4(decode)": blk_op, "k_rs_jit12x4(decode)": blk_op, "k_rs_jit10x4(decode)": blk_op,
             "k_decode_prepare": 0.0, "k_decode_prepare_syn": 0.0}
 
 
@@ -753,14 +761,15 @@ def main(argv=None):
         extra = {"launch": dict(launch_cost(torch), launches_per_step=round(len(recs) / steps, 2),
                                 step_us=round(ms_step * 1e3, 2))}
 
-    per, kernels = kernel_stats(recs, steps, alg)
+    # this rank's blocks per step (C4: its share of the stream)
+    per, kernels = kernel_stats(recs, steps, alg, out_bytes_step / (2.0 * e * L) if args.config != "c4" else share)
     # dominant kernel = the most device time per step
     dom = max(per, key=lambda n: per[n][0])
-    tot, n, nb = per[dom]
+    tot, n, nb, passes = per[dom]
     dom_ms = tot / n
-    dom_bytes = alg.get(dom, 0.0) * nb / n      # algorithmic bytes per launch
+    dom_bytes = alg.get(dom, 0.0) * nb / n / passes  # algorithmic bytes per launch
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
-    read_bytes = float(k * L) * nb / n if alg.get(dom, 0.0) else 0.0
+    read_bytes = float(k * L) * nb / n / passes if alg.get(dom, 0.0) else 0.0
     # PMC bytes per launch come from a separate rocprofv3 --pmc pass of the
     # same command (counters cannot be read inside this timed run); only
     # valid for the C3 workload they were measured on

@@ -302,32 +302,36 @@ std::vector<uint8_t> build_matrix_code_wide(const uint8_t* c, int k, int e, int 
 {
     const int nch = (k + CS - 1) / CS;
     // programs of every (wave, source), then the chunk sizes
-    std::vector<SrcProg> progs((size_t)2 * k);
-    for (int w = 0; w < 2; ++w) {
-        const int nslot = std::min(R, e - R * w);
+    const int nv = wide_waves(e);
+    auto row0 = [&](int w) { return wide_row0(e, w); };
+    if ((e + nv - 1) / nv > R || R > kMaxSlots)  // a wave's rows exceed its accumulators
+        return {};
+    std::vector<SrcProg> progs((size_t)nv * k);
+    for (int w = 0; w < nv; ++w) {
+        const int nslot = row0(w + 1) - row0(w);
         for (int q = 0; q < k && nslot > 0; ++q) {
             uint8_t cf[kMaxSlots];
             for (int s = 0; s < nslot; ++s)
-                cf[s] = c[(size_t)(R * w + s) * k + q];
+                cf[s] = c[(size_t)(row0(w) + s) * k + q];
             plan_source(cf, nslot, progs[(size_t)w * k + q], max_ops);
         }
     }
     size_t most = 0;
-    for (int w = 0; w < 2; ++w) {
-        const int nslot = std::min(R, e - R * w);
+    for (int w = 0; w < nv; ++w) {
+        const int nslot = row0(w + 1) - row0(w);
         for (int ch = 0; ch < nch && nslot > 0; ++ch)
             most = std::max(most, emit_chunk_wide(nullptr, std::min(CS, k - CS * ch), nslot,
                                                   &progs[(size_t)w * k + CS * ch]));
     }
     const int stride = (int)((most + 63) / 64 * 64);
     *chunk_stride = stride;
-    std::vector<uint8_t> code((size_t)2 * nch * stride);
+    std::vector<uint8_t> code((size_t)nv * nch * stride);
     for (size_t i = 0; i + 8 <= code.size(); i += 8) {
         const uint64_t ret = (uint64_t)S_NOP0 << 32 | S_SETPC_82;
         memcpy(&code[i], &ret, 8);
     }
-    for (int w = 0; w < 2; ++w) {
-        const int nslot = std::min(R, e - R * w);
+    for (int w = 0; w < nv; ++w) {
+        const int nslot = row0(w + 1) - row0(w);
         for (int ch = 0; ch < nch && nslot > 0; ++ch)
             emit_chunk_wide(&code[((size_t)w * nch + ch) * stride], std::min(CS, k - CS * ch), nslot,
                             &progs[(size_t)w * k + CS * ch]);

@@ -195,11 +195,16 @@ RJ_HD inline bool code_word(const uint8_t* rows, int k, int nslot, int ch, int o
 //   R = 10 (k_rs_jit10, 16 < e <= 20): 80 accumulators, 120 VGPRs, 4 waves
 //          per SIMD, chunks of 5 sources (8 workgroups per CU); composites
 //          twice per source and tile instead of three times (8 + 8 + 4 rows)
-// Register contract (both):
+// Four waves per column tile for 32 < e <= 64 (R = 10 / 12 / 16 for e up to
+// 40 / 48 / 64), so a tile's sources are loaded and transposed once for all
+// e rows (the 8-row layout runs passes of 32 rows, each reading every source).
+// Wave w of NV = wide_waves(e) holds rows wide_row0(e, w) .. wide_row0(e, w + 1)
+// - 1 (balanced: at most one row apart).
+// Register contract (all):
 //   v9             LDS byte address of the chunk's first source + 16 lane
 //   v10..v17       planes of the current source: L1 L2 L4 L8 H1 H2 H4 H8
 //   v18..v28       composites L[n], n = 3 5 6 7 9 ... 15; v29..v39 H[n]
-//   v40..v40+8R-1  accumulators: slot s (row R w + s) plane b at v40+8s+b
+//   v40..v40+8R-1  accumulators: slot s (row wide_row0(e, w) + s) plane b at v40+8s+b
 //   s[82:83]       return address
 // Code of one chunk (nt <= CS sources, nslot <= R rows of the wave):
 //   source t   ds_read_b128 x2 of its own planes, s_waitcnt lgkmcnt(0), the
@@ -208,6 +213,9 @@ RJ_HD inline bool code_word(const uint8_t* rows, int k, int nslot, int ch, int o
 //   epilogue   s_setpc_b64 s[82:83]; s_nop                           8 B
 // No next-source prefetch (no register bank for it): the other waves of the
 // SIMD cover the LDS latency.
+RJ_HD constexpr int wide_waves(int e) { return e > 32 ? 4 : 2; }
+RJ_HD constexpr int wide_row0(int e, int w) { return w * e / wide_waves(e); }
+
 template <int R_, int CS_>
 struct Wide {
     static constexpr int R = R_, CS = CS_;

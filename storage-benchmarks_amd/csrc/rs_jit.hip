@@ -254,17 +254,19 @@ __device__ __forceinline__ void read_slotw(uint32_t (&W)[8])
 // not allocate them itself, and the kernel descriptor still gives the wave
 // 168 VGPRs (.amdhsa_next_free_vgpr 168, no AGPRs), which only the asm and
 // the generated code touch.
-// TPW > 1: one workgroup covers TPW consecutive column tiles of a block (2
+// NV = 4 (e > 32): four waves per tile, the same chunk of sources in LDS for
+// all of them (rs_jit.h wide_waves / wide_row0), one tile per workgroup.
+// TPW > 1 (NV = 2): one workgroup covers TPW consecutive column tiles of a block (2
 // TPW waves; wave w: tile w / 2, rows of wave w % 2), so the TPW waves with
 // the same rows run the same code between the same chunk barriers and share
 // its instruction-cache lines.
-template <class W, int TPW>
-__global__ __launch_bounds__(128 * TPW) __attribute__((amdgpu_num_vgpr(40))) void k_rs_jitw(JitArgs a)
+template <class W, int TPW, int NV>
+__global__ __launch_bounds__(64 * NV * TPW) __attribute__((amdgpu_num_vgpr(40))) void k_rs_jitw(JitArgs a)
 {
     constexpr int CS = W::CS, R = W::R;
     __shared__ uint4 lds[2][TPW][CS * 2 * 64];
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int wave = wv & 1, tw = wv >> 1;  // rows of the wave, its tile in the workgroup
+    const int wave = wv % NV, tw = wv / NV;  // rows of the wave, its tile in the workgroup
     const int lane = threadIdx.x & 63;
     int b = blockIdx.y;
     long long tile = blockIdx.x;
@@ -295,19 +297,19 @@ __global__ __launch_bounds__(128 * TPW) __attribute__((amdgpu_num_vgpr(40))) voi
     // use (one s_load + wait per source measured 5-7 % of the wave's time)
     typedef const uint8_t* const __attribute__((address_space(4)))* CPtrs;
     const CPtrs csrcs = (CPtrs)srcs;
-    constexpr int PW = (CS + 1) / 2;  // this wave's sources per chunk: t = wave, wave + 2, ...
+    constexpr int PW = (CS + NV - 1) / NV;  // this wave's sources per chunk: t = wave, wave + NV, ...
     auto ptrs = [&](int ch, const uint8_t* (&p)[PW]) {
         const int c0 = ch * CS, nt = min(CS, k - c0);
 #pragma unroll
         for (int i = 0; i < PW; ++i)
-            p[i] = csrcs[c0 + min(wave + 2 * i, nt - 1)];  // in bounds, unconditional
+            p[i] = csrcs[c0 + min(wave + NV * i, nt - 1)];  // in bounds, unconditional
     };
     auto issue = [&](int ch, const uint8_t* const (&p)[PW]) {
         const int c0 = ch * CS, nt = min(CS, k - c0);
         const uint32_t base = lds0 + (uint32_t)((ch & 1) * kBuf);
 #pragma unroll
         for (int i = 0; i < PW; ++i) {
-            const int t = wave + 2 * i;
+            const int t = wave + NV * i;
             if (t < nt)
                 glds32(p[i], loff, base + (uint32_t)(t * 2 * 64 * 16));
         }
@@ -329,9 +331,9 @@ __global__ __launch_bounds__(128 * TPW) __attribute__((amdgpu_num_vgpr(40))) voi
         // instruction fetch, which misses line by line, finds it there; the
         // wait also covers the sources just issued, needed next anyway
         const uint8_t* cb = a.code + (size_t)b * a.block_stride;
-        const long long lines = (2LL * nch * a.chunk_stride) >> 7;
+        const long long lines = ((long long)NV * nch * a.chunk_stride) >> 7;
         const long long lo = wg * lines / gridDim.x, hi = (wg + 1) * lines / gridDim.x;
-        for (long long i = lo + threadIdx.x; i < hi; i += 128 * TPW) {
+        for (long long i = lo + threadIdx.x; i < hi; i += 64 * NV * TPW) {
             uint32_t d;
             asm volatile("global_load_dword %0, %1, off\n s_waitcnt vmcnt(0)" : "=v"(d) : "v"(cb + (i << 7)) : "memory");
         }
@@ -342,7 +344,7 @@ __global__ __launch_bounds__(128 * TPW) __attribute__((amdgpu_num_vgpr(40))) voi
         wait_vm(0);
         {
             const uint32_t m4 = vconst(0x0F0F0F0Fu), m2 = vconst(0x33333333u), m1 = vconst(0x55555555u);
-            for (int t = wave; t < nt; t += 2) {
+            for (int t = wave; t < nt; t += NV) {
                 uint4 u = buf[(t * 2 + 0) * 64 + lane], v = buf[(t * 2 + 1) * 64 + lane];
                 uint32_t Wd[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
                 tr8(Wd, m4, m2, m1);
@@ -374,17 +376,17 @@ __global__ __launch_bounds__(128 * TPW) __attribute__((amdgpu_num_vgpr(40))) voi
     }
     // the output pointers likewise: all R loads under one wait
     typedef uint8_t* const __attribute__((address_space(4)))* CDsts;
+    const int r0 = jit::wide_row0(a.rows, wave), nrow = jit::wide_row0(a.rows, wave + 1) - r0;
     uint8_t* dp[R];
 #pragma unroll
     for (int i = 0; i < R; ++i)
-        dp[i] = ((CDsts)dsts)[min(wave * R + i, a.rows - 1)];
+        dp[i] = ((CDsts)dsts)[min(r0 + i, a.rows - 1)];
     if (off + 32 <= a.len) {
         const uint32_t m4 = vconst(0x0F0F0F0Fu), m2 = vconst(0x33333333u), m1 = vconst(0x55555555u);
         [&]<int... Ss>(std::integer_sequence<int, Ss...>) {
             (
                 [&] {
-                    const int r = wave * R + Ss;
-                    if (r < a.rows) {
+                    if (Ss < nrow) {
                         uint32_t Wd[8];
                         read_slotw<Ss>(Wd);
                         tr8(Wd, m4, m2, m1);
@@ -465,7 +467,7 @@ __global__ __launch_bounds__(256) void k_jit_emit(int k, int e, const uint8_t* c
 __constant__ jit::WideTables kWideTab = jit::wide_tables();
 
 // k_rs_jitw<R>'s code (rs_jit.h Wide), one workgroup per (block, wave) as
-// k_jit_emit: rows R w .. R w + R - 1 of the block's decode rows.  Each word
+// k_jit_emit: rows wide_row0(e, w) .. wide_row0(e, w + 1) - 1 of the block's decode rows.  Each word
 // is a table entry (the coefficient's matrix row and register operands are
 // fixed per (c, plane)) with the accumulator ORed in: per 16 bytes of code
 // one 16-byte table load, two selects and ORs.  (Computing every word from
@@ -482,14 +484,14 @@ __global__ __launch_bounds__(256) void k_jitw_emit(int k, int e, const uint8_t* 
     if (status[b] != 0)
         return;
     const int nch = (k + CS - 1) / CS;
-    const int nslot = min(R, e - R * w);
+    const int r0 = jit::wide_row0(e, w), nslot = jit::wide_row0(e, w + 1) - r0;
     const size_t stride = (size_t)W::chunk_stride();
-    uint8_t* cbase = code + ((size_t)b * 2 + w) * nch * stride;
+    uint8_t* cbase = code + ((size_t)b * jit::wide_waves(e) + w) * nch * stride;
     const int sb = W::src_bytes(nslot);
     // every load of a phase in flight before its first use: the loops below
     // would otherwise wait a full memory latency per iteration
     {
-        const uint8_t* cr = coef + ((size_t)b * e + R * w) * k;
+        const uint8_t* cr = coef + ((size_t)b * e + r0) * k;
         constexpr int NB = R * 256 / 256;  // bytes per thread, nslot * k <= R * 250
         uint8_t v[NB];
 #pragma unroll
@@ -552,7 +554,12 @@ __global__ __launch_bounds__(256) void k_jitw_emit(int k, int e, const uint8_t* 
 }
 
 // rows per wave of the 2-wave layout for e rows, 0 = the 8-row layout
-int jitw_rows(int e) { return e > 24 && e <= 32 ? 16 : e > 20 && e <= 24 ? 12 : e > 16 && e <= 20 ? 10 : 0; }
+int jitw_rows(int e)
+{
+    if (e > 32)  // four waves
+        return e > 48 && e <= 64 ? 16 : e > 40 && e <= 64 ? 12 : e > 32 && e <= 64 ? 10 : 0;
+    return e > 24 ? 16 : e > 20 ? 12 : e > 16 ? 10 : 0;
+}
 
 size_t jitw_chunk_stride(int e)
 {
@@ -564,7 +571,7 @@ size_t jitw_code_bytes(int k, int e, long long blocks)
 {
     const int r = jitw_rows(e);
     const int cs = r == 16 ? jit::J16::CS : r == 12 ? jit::J12::CS : jit::J10::CS;
-    return (size_t)blocks * 2 * ((k + cs - 1) / cs) * jitw_chunk_stride(e);
+    return (size_t)blocks * jit::wide_waves(e) * ((k + cs - 1) / cs) * jitw_chunk_stride(e);
 }
 
 hipError_t launch_jitw_emit(int k, int e, long long blocks, const uint8_t* coef, const int* status,
@@ -573,13 +580,13 @@ hipError_t launch_jitw_emit(int k, int e, long long blocks, const uint8_t* coef,
     if (k <= 0 || k > 250 || !jitw_rows(e) || k + e > 250 || blocks <= 0 || !coef || !status || !code)
         return hipErrorInvalidValue;
     if (jitw_rows(e) == 16)
-        hipLaunchKernelGGL(k_jitw_emit<jit::J16>, dim3(2, (unsigned)blocks), dim3(256), 0, st, k, e, coef, status,
+        hipLaunchKernelGGL(k_jitw_emit<jit::J16>, dim3(jit::wide_waves(e), (unsigned)blocks), dim3(256), 0, st, k, e, coef, status,
                            code);
     else if (jitw_rows(e) == 12)
-        hipLaunchKernelGGL(k_jitw_emit<jit::J12>, dim3(2, (unsigned)blocks), dim3(256), 0, st, k, e, coef, status,
+        hipLaunchKernelGGL(k_jitw_emit<jit::J12>, dim3(jit::wide_waves(e), (unsigned)blocks), dim3(256), 0, st, k, e, coef, status,
                            code);
     else
-        hipLaunchKernelGGL(k_jitw_emit<jit::J10>, dim3(2, (unsigned)blocks), dim3(256), 0, st, k, e, coef, status,
+        hipLaunchKernelGGL(k_jitw_emit<jit::J10>, dim3(jit::wide_waves(e), (unsigned)blocks), dim3(256), 0, st, k, e, coef, status,
                            code);
     return hipGetLastError();
 }
@@ -588,16 +595,22 @@ hipError_t launch_rs_jitw(const JitArgs& a, long long blocks, hipStream_t st)
 {
     if (!jitw_rows(a.rows) || a.dst_stride < a.rows || a.k <= 0 || !a.code || a.chunk_stride <= 0)
         return hipErrorInvalidValue;
-    const int tpw = a.tiles_per_wg >= 3 ? 3 : a.tiles_per_wg == 2 ? 2 : 1;
+    // four waves per tile (e > 32): one tile per workgroup, three 4-wave
+    // workgroups fill a CU's 12 wave slots
+    const int nv = jit::wide_waves(a.rows);
+    const int tpw = nv == 4 ? 1 : a.tiles_per_wg >= 3 ? 3 : a.tiles_per_wg == 2 ? 2 : 1;
     const long long ntile = (a.len + 2047) / 2048;
     dim3 grid((unsigned)((ntile + tpw - 1) / tpw), (unsigned)blocks);
-    dim3 blk(128 * tpw);
+    dim3 blk(64 * nv * tpw);
 #define RSGPU_JW_LAUNCH(WT)                                                                          \
-    switch (tpw) {                                                                                   \
-    case 3: hipLaunchKernelGGL((jitk::k_rs_jitw<WT, 3>), grid, blk, 0, st, a); break;               \
-    case 2: hipLaunchKernelGGL((jitk::k_rs_jitw<WT, 2>), grid, blk, 0, st, a); break;               \
-    default: hipLaunchKernelGGL((jitk::k_rs_jitw<WT, 1>), grid, blk, 0, st, a); break;              \
-    }
+    if (nv == 4)                                                                                     \
+        hipLaunchKernelGGL((jitk::k_rs_jitw<WT, 1, 4>), grid, blk, 0, st, a);                        \
+    else                                                                                             \
+        switch (tpw) {                                                                               \
+        case 3: hipLaunchKernelGGL((jitk::k_rs_jitw<WT, 3, 2>), grid, blk, 0, st, a); break;        \
+        case 2: hipLaunchKernelGGL((jitk::k_rs_jitw<WT, 2, 2>), grid, blk, 0, st, a); break;        \
+        default: hipLaunchKernelGGL((jitk::k_rs_jitw<WT, 1, 2>), grid, blk, 0, st, a); break;       \
+        }
     if (jitw_rows(a.rows) == 16) {
         RSGPU_JW_LAUNCH(jit::J16)
     } else if (jitw_rows(a.rows) == 12) {

@@ -269,9 +269,9 @@ template <class W>
 void jitw_emit_host(int k, int e, const unsigned char* coef, uint64_t* o64)
 {
     const int nch = (k + W::CS - 1) / W::CS, stride_w = W::chunk_stride() / 8;
-    for (int w = 0; w < 2; ++w) {
-        const int nslot = std::min(W::R, e - W::R * w);
-        const unsigned char* rows = coef + (size_t)W::R * w * k;
+    for (int w = 0; w < jit::wide_waves(e); ++w) {
+        const int r0 = jit::wide_row0(e, w), nslot = jit::wide_row0(e, w + 1) - r0;
+        const unsigned char* rows = coef + (size_t)r0 * k;
         for (int ch = 0; ch < nch; ++ch)
             for (int o = 0; o < stride_w; ++o) {
                 uint64_t word;
@@ -284,8 +284,9 @@ void jitw_emit_host(int k, int e, const unsigned char* coef, uint64_t* o64)
 int jitw_cs(int e) { return jitw_rows(e) == 16 ? jit::J16::CS : jitw_rows(e) == 12 ? jit::J12::CS : jit::J10::CS; }
 
 // The shared program of a matrix (jit_prog.h, composites by greedy cover):
-// for 16 < rows <= 32 in the two-wave layout of the decode (k_rs_jitw: a
-// source's composites built twice per tile), else the 8-row layout (k_rs_jit).
+// for 16 < rows <= 64 in the two- / four-wave layout of the decode (k_rs_jitw: a
+// source's composites built twice or four times per tile), else the 8-row
+// layout (k_rs_jit).
 int shared_program(rsgpu_ctx* ctx, const uint8_t* coef, int k, int rows)
 {
     const bool wide = jitw_rows(rows) != 0;
@@ -1152,7 +1153,7 @@ int jit_decode_launch(rsgpu_ctx* ctx, int k, int e, size_t len, size_t blocks, c
         // their code's instruction-cache lines (C4 13.7 vs 14.2 ms per 16384
         // blocks, C3 23.2-23.3 vs 23.4-23.5, C5 12.7-12.8 vs 12.8-12.9;
         // three tiles: 20-30 % slower; profiles/r03_ab/tpw/)
-        j.tiles_per_wg = ctx->jitw_tpw ? ctx->jitw_tpw : 2;
+        j.tiles_per_wg = jit::wide_waves(e) == 4 ? 1 : ctx->jitw_tpw ? ctx->jitw_tpw : 2;
         // short rows: the block's few workgroups pull its code into L2 before
         // the instruction fetch misses on it line by line (C4: 12.8 vs 13.7
         // ms per 16384 blocks; C3, 245 workgroups per block, unchanged:
@@ -1163,7 +1164,10 @@ int jit_decode_launch(rsgpu_ctx* ctx, int k, int e, size_t len, size_t blocks, c
             j.code_prefetch = ctx->jitw_prefetch >= 0 ? ctx->jitw_prefetch : lines >= 32 * wgs;
         }
         KTimer kt(ctx,
-                  jitw_rows(e) == 16   ? "k_rs_jit16(decode)"
+                  e > 32 ? (jitw_rows(e) == 16   ? "k_rs_jit16x4(decode)"
+                            : jitw_rows(e) == 12 ? "k_rs_jit12x4(decode)"
+                                                 : "k_rs_jit10x4(decode)")
+                  : jitw_rows(e) == 16 ? "k_rs_jit16(decode)"
                   : jitw_rows(e) == 12 ? "k_rs_jit12(decode)"
                                        : "k_rs_jit10(decode)",
                   blocks);
@@ -1575,8 +1579,8 @@ long long rsgpu_internal_jit_emit(int k, int e, const unsigned char* coef, unsig
     return (long long)need;
 }
 
-// Test hook (not part of include/rsgpu.h): the same for the two-wave layouts
-// of k_rs_jitw (rs_jit.h Wide, R = 16 for 24 < e <= 32, 10 for 16 < e <= 20),
+// Test hook (not part of include/rsgpu.h): the same for the two- and
+// four-wave layouts of k_rs_jitw (rs_jit.h Wide, jitw_rows, wide_waves),
 // from Wide::code_word (the words k_jitw_emit writes).
 long long rsgpu_internal_jitw_emit(int k, int e, const unsigned char* coef, unsigned char* out,
                                    size_t out_bytes)
@@ -1599,7 +1603,7 @@ long long rsgpu_internal_jitw_emit(int k, int e, const unsigned char* coef, unsi
 }
 
 // Test hook (not in include/rsgpu.h): the host-built shared program of an
-// e x k matrix in the two-wave layout (16 < e <= 32), for the CPU suite to
+// e x k matrix in the two- or four-wave layout (16 < e <= 64), for the CPU suite to
 // disassemble and interpret.  Returns the bytes needed, or -1; writes only
 // when out_bytes is large enough; *chunk_stride gets the stride.
 long long rsgpu_internal_jitw_matrix_code(int k, int e, const unsigned char* coef, unsigned char* out,

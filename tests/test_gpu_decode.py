@@ -85,8 +85,10 @@ def decode_poisoned(ctx, enc, dec):
 GEOMS = [(16, 4, 1000000, 2), (64, 32, 1000000, 2), (100, 20, 1000000, 2), (16, 8, 64000, 4),
          (64, 32, 32000, 16), (40, 20, 8192, 3), (200, 32, 2048, 2), (128, 64, 4096, 2),
          (12, 12, 512, 2), (33, 1, 64, 2),
-         # 32 < e <= 63: closed-form rows, generated code in passes of 32 rows
-         (96, 48, 131072, 2), (187, 63, 4096, 2), (40, 33, 98304, 2),
+         # 32 < e <= 64: closed-form rows (e <= 63) or the k x k inversion,
+         # generated code in four waves per tile (k_rs_jit{10,12,16}x4)
+         (96, 48, 131072, 2), (187, 63, 4096, 2), (40, 33, 98304, 2), (100, 50, 131072, 2),
+         (128, 64, 131072, 2), (70, 45, 65536, 3),
          # 24 < e <= 32: 16 rows per wave (k_rs_jit16) when generated;
          # 16 < e <= 20: 10 rows per wave (k_rs_jit10)
          (50, 25, 98304, 3), (31, 31, 4096, 2), (218, 32, 2048, 2),
@@ -102,7 +104,7 @@ def test_poisoned_decode_every_kernel(ctx, kernel, k, e, L, B):
     general k x k inversion, and the automatic choice) recovers the
     originals with the erased rows poisoned, at the BASELINE geometries
     (C2, C3, C5, C1 golden, C4) and general codes (k up to 200, e up to 64
-    via row passes, e == k)."""
+    in four waves per tile, e == k)."""
     ctx.set_decode_kernel(kernel)
     try:
         enc = rsgpu.GpuEncoder(k, L, e, blocks=B, seed=17, ctx=ctx)
@@ -718,7 +720,7 @@ def test_jitw_code_prefetch(ctx, k, e, L, B):
 
 
 @pytest.mark.parametrize("k,e", [(64, 32), (25, 25), (218, 32), (48, 24), (21, 21), (100, 20), (17, 17),
-                                 (230, 20)])
+                                 (230, 20), (100, 50), (128, 64), (70, 45), (40, 33)])
 def test_device_emitter_writes_the_host_emitters_code(ctx, k, e):
     """k_jitw_emit (table-driven, on the device) writes, block for block and
     word for word, the code of the host emitter Wide::code_word, which the

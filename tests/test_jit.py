@@ -240,6 +240,22 @@ def test_shared_matrix_code(k, e, kind):
         assert n_comp / n_src < 18, n_comp / n_src
 
 
+def wide_rows(e):
+    """jitw_rows: accumulator rows per wave of the two- / four-wave layouts."""
+    if e > 32:
+        return 16 if e > 48 else 12 if e > 40 else 10
+    return 16 if e > 24 else 12 if e > 20 else 10
+
+
+def wide_waves(e):
+    return 4 if e > 32 else 2
+
+
+def wide_row0(e, w):
+    """rs_jit.h wide_row0: wave w's first row (balanced split)."""
+    return w * e // wide_waves(e)
+
+
 def matrix_code_wide(k, e, coef, max_ops=22):
     import rsgpu
     f = rsgpu.lib().rsgpu_internal_jitw_matrix_code
@@ -255,16 +271,17 @@ def matrix_code_wide(k, e, coef, max_ops=22):
 
 @pytest.mark.parametrize("k,e,kind", [(64, 32, "rs"), (100, 20, "rs"), (100, 25, "random"),
                                       (128, 32, "random"), (48, 24, "random"), (17, 17, "random"),
-                                      (24, 17, "capped"), (218, 32, "rs")])
+                                      (24, 17, "capped"), (218, 32, "rs"), (100, 50, "rs"),
+                                      (128, 64, "random"), (60, 40, "random"), (40, 33, "capped")])
 def test_shared_matrix_code_wide(k, e, kind):
-    """The GENERATED encode's host-built code for 16 < e <= 32 in the
-    decode's two-wave layout (jit_prog.cpp build_matrix_code_wide: planes
+    """The GENERATED encode's host-built code for 16 < e <= 64 in the
+    decode's two- / four-wave layout (jit_prog.cpp build_matrix_code_wide: planes
     v10..v17 from LDS at v9, covered composites from v18, accumulators from
     v40): interpreted chunk by chunk, every accumulator equals sum_q c[row][q]
     * src_q over GF(2^8), registers stay in v9..v(40+8R-1), every register is
     read after its LDS load was waited for, and the covers average under the
     22 composites of the full tables."""
-    R = 16 if e > 24 else 12 if e > 20 else 10
+    R, nv = wide_rows(e), wide_waves(e)
     cs = WIDE[R][0]
     rng = random.Random(k * 1000 + e)
     if kind == "rs":
@@ -274,11 +291,12 @@ def test_shared_matrix_code_wide(k, e, kind):
         coef[0, 0] = 0
     code, stride = matrix_code_wide(k, e, coef, 6 if kind == "capped" else 22)
     nch = (k + cs - 1) // cs
-    assert stride % 64 == 0 and len(code) == 2 * nch * stride
+    assert stride % 64 == 0 and len(code) == nv * nch * stride
     src = [[rng.randrange(256) for _ in range(32)] for _ in range(k)]
     n_comp = n_src = 0
-    for w in range(2):
-        nslot = min(R, e - R * w)
+    for w in range(nv):
+        nslot = wide_row0(e, w + 1) - wide_row0(e, w)
+        assert 0 < nslot <= R
         regs = {r: 0 for r in range(256)}
         pending = []
         for ch in range(nch):
@@ -301,7 +319,7 @@ def test_shared_matrix_code_wide(k, e, kind):
             run_chunk(ins, regs, lds, pending, addr_reg="v9")
             assert not pending, "a load left outstanding at the return"
         for s in range(nslot):
-            row = R * w + s
+            row = wide_row0(e, w) + s
             want = [0] * 32
             for q in range(k):
                 want = [x ^ g.gf_mul(int(coef[row, q]), y) for x, y in zip(want, src[q])]
@@ -332,25 +350,27 @@ WIDE = {16: (6, 6848), 12: (6, 5312), 10: (5, 3776)}
 
 
 @pytest.mark.parametrize("k,e", [(64, 32), (25, 25), (100, 30), (13, 27), (218, 32),
-                                 (100, 20), (17, 17), (64, 19), (230, 20), (48, 24), (21, 21), (226, 24)])
+                                 (100, 20), (17, 17), (64, 19), (230, 20), (48, 24), (21, 21), (226, 24),
+                                 (100, 50), (128, 64), (186, 64), (60, 40), (70, 45), (40, 33)])
 def test_generated_wide_block_decodes(k, e):
-    """k_rs_jitw's code (rs_jit.h Wide: 2 waves x R rows, R = 16 for
-    24 < e <= 32 and 10 for 16 < e <= 20, chunks of CS sources, each source
+    """k_rs_jitw's code (rs_jit.h Wide: 2 waves x R rows for e <= 32, 4
+    waves for 32 < e <= 64, rows split evenly, chunks of CS sources, each source
     loading its own planes, accumulators from v40): every accumulator equals
     sum_q c[row][q] * src_q over GF(2^8), only the allowed instructions
     appear, every register is read after its LDS load was waited for, and
     each chunk returns right after its last source."""
-    R = 16 if e > 24 else 12 if e > 20 else 10
+    R, nv = wide_rows(e), wide_waves(e)
     cs, stride = WIDE[R]
     rng = random.Random(k * 7 + e)
     coef = np.array([[rng.randrange(256) for _ in range(k)] for _ in range(e)], np.uint8)
     coef[1, 2] = 0
     code = emitw(k, e, coef).tobytes()
     nch = (k + cs - 1) // cs
-    assert len(code) == 2 * nch * stride
+    assert len(code) == nv * nch * stride
     src = [[rng.randrange(256) for _ in range(32)] for _ in range(k)]
-    for w in range(2):
-        nslot = min(R, e - R * w)
+    for w in range(nv):
+        nslot = wide_row0(e, w + 1) - wide_row0(e, w)
+        assert 0 < nslot <= R
         regs = {r: 0 for r in range(256)}
         pending = []
         for ch in range(nch):
@@ -370,7 +390,7 @@ def test_generated_wide_block_decodes(k, e):
             used += [int(n) for _, _, ops in ins for n in re.findall(r"v\[\d+:(\d+)\]", ops)]
             assert max(used) < 40 + 8 * R and min(used) >= 9, "register outside the kernel's v9..v(40+8R-1)"
         for s in range(nslot):
-            row = R * w + s
+            row = wide_row0(e, w) + s
             want = [0] * 32
             for q in range(k):
                 want = [x ^ g.gf_mul(int(coef[row, q]), y) for x, y in zip(want, src[q])]
