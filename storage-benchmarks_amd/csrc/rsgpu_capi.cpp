@@ -1009,6 +1009,17 @@ constexpr size_t kJitwMinTiles = 16;
 constexpr size_t kJitXcdTiles = 128;
 
 size_t jit_min_tiles(int e) { return jitw_rows(e) ? kJitwMinTiles : kJitMinTiles; }
+size_t decode_code_bytes(int k, int e, size_t blocks);
+// generated code pays for a block of `tiles` column tiles: enough tiles to
+// amortise its code (every tile's workgroup fetches all of it), or code so
+// small that fetching it per tile costs little: (16, 8, 32000), 16 tiles and
+// 10 KB of code per block, decodes in 3.38 + 0.08 ms emission per 16384
+// blocks against 3.72 threaded (profiles/r03_ab/k16s32k/)
+constexpr size_t kJitCodePerTile = 1024;
+bool jit_pays(int k, int e, size_t tiles)
+{
+    return tiles >= jit_min_tiles(e) || decode_code_bytes(k, e, 1) <= kJitCodePerTile * tiles;
+}
 // (block, tile) pairs per call from which AUTO pays the emission launch
 // (~10 us whatever the batch) for the ~4 ns per pair the generated code saves
 // over threaded code: C2 (one block, 489 tiles) decodes 16 us threaded
@@ -1041,7 +1052,7 @@ Plan decode_plan(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch, size_t 
     // (e <= 63); the threaded-code kernel takes e <= 32
     const bool gen_ok = e <= 63 && jit_probe(ctx) == 1 && want != RSGPU_DECODE_ONE_MATRIX &&
                         want != RSGPU_DECODE_GENERAL &&
-                        (want == RSGPU_DECODE_GENERATED || (len + 2047) / 2048 >= jit_min_tiles(e));
+                        (want == RSGPU_DECODE_GENERATED || jit_pays(k, e, (len + 2047) / 2048));
     if (e > 32 && gen_ok)
         return Plan::generated;
     if (want == RSGPU_DECODE_GENERAL || e > 32)
@@ -1054,7 +1065,7 @@ Plan decode_plan(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch, size_t 
     // 128000 (63 tiles) 3.79 vs 3.94 ms (8-row layout, profiles/r02_ab); C4
     // (16 tiles) with two tiles per workgroup, above
     if (want == RSGPU_DECODE_AUTO &&
-        ((len + 2047) / 2048 < jit_min_tiles(e) || (len + 2047) / 2048 * blocks < kJitMinWork))
+        (!jit_pays(k, e, (len + 2047) / 2048) || (len + 2047) / 2048 * blocks < kJitMinWork))
         return Plan::one_matrix;
     return Plan::generated;
 }

@@ -494,6 +494,28 @@ def test_auto_decode_kernel_by_batch_work(ctx, blocks, name):
     assert name in names and names[-1] == name, names
 
 
+@pytest.mark.parametrize("k,e,name", [(16, 8, "k_rs_jit(decode)"), (64, 16, "k_rs_tc(decode)"),
+                                      (64, 32, "k_rs_jit16(decode)")])
+def test_auto_decode_short_rows_by_code_size(ctx, k, e, name):
+    """Short rows (32000 bytes, 16 column tiles per block; README.rst:130-133
+    sweeps symbol_size 32000): AUTO takes generated code where a block's code
+    is small per tile ((16, 8): 10 KB) or the two-wave layout pays ((64, 32)),
+    threaded code where 80 KB of 8-row code would be fetched by each of 16
+    tiles ((64, 16)); erased rows poisoned."""
+    L, B = 32000, 256
+    ctx.set_decode_kernel("auto")
+    enc = rsgpu.GpuEncoder(k, L, e, blocks=B, seed=31, ctx=ctx)
+    enc.encode_all()
+    dec = rsgpu.GpuDecoder(k, L, e, blocks=B, seed=31, ctx=ctx)
+    ctx.timing_read()
+    ctx.timing_enable(True)
+    ok = decode_poisoned(ctx, enc, dec)
+    names = [n for n, _, _ in ctx.timing_read()]
+    ctx.timing_enable(False)
+    assert ok and dec.verify_data(enc)
+    assert names[-1] == name, names
+
+
 def test_generated_apply_checks_its_prepare(ctx):
     """The generated decode keeps ONE prepare's code per context: prepare(A),
     prepare(B), apply(A) must fail (RSGPU_ERR_ARG, nothing launched) instead
