@@ -151,10 +151,10 @@ size_t rsgpu_decode_workspace_bytes(int k, int e, size_t blocks);
 
 /* Decode kernel of rsgpu_decode_blocks (per context; every choice recovers
  * the same bytes):
- *   AUTO        GENERATED when a block has >= 48 column tiles of 2 KB
- *               (len > 94 KiB; >= 16 tiles, len > 30 KiB, for 16 < e <= 32)
- *               and the call has >= 4096 (block, tile) pairs, else
- *               ONE_MATRIX (the default)
+ *   AUTO        GENERATED when a block has >= 16 column tiles of 2 KB
+ *               (len > 30 KiB), or fewer whose generated code is at most
+ *               6 KB per tile, and the call has >= 4096 (block, tile)
+ *               pairs, else ONE_MATRIX (the default)
  *   ONE_MATRIX  closed-form e x k decode rows V_E^-1 [V_kept | I] (e <= 32),
  *               one threaded-code pass over the k - e survivors + e parity;
  *               rsgpu_decode_blocks runs a small call (< 2048 (block, 2 KB

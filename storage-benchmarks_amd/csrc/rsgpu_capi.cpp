@@ -1000,22 +1000,25 @@ enum class Plan {
 };
 
 // column tiles (2 KB) per block from which AUTO decodes through generated
-// code (the two-wave layouts, 16 < e <= 32, run two tiles per workgroup and
-// pay from 16 tiles: C4 14.07 + 0.86 emission vs 15.44 ms threaded per 16384
-// blocks, profiles/r03_ab/c4_gen_vs_tc/); below kJitXcdTiles the 8-row
-// decode runs in XCD-contiguous order
-constexpr size_t kJitMinTiles = 48;
+// code, every layout: the two-wave layouts (16 < e <= 32, two tiles per
+// workgroup) pay from 16 tiles (C4 14.07 + 0.86 emission vs 15.44 ms
+// threaded per 16384 blocks, profiles/r03_ab/c4_gen_vs_tc/), and so does the
+// 8-row layout in XCD-contiguous order (per 16384 / 8192 blocks of 16 tiles,
+// profiles/r03_ab/autoshort/: (64, 16) 10.69 + 0.54 vs 12.06 ms, (128, 16)
+// 9.90 + 0.52 vs 11.82; round 2 measured 48 tiles, before that order); below
+// kJitXcdTiles the 8-row decode runs in XCD-contiguous order
+constexpr size_t kJitMinTiles = 16;
 constexpr size_t kJitwMinTiles = 16;
 constexpr size_t kJitXcdTiles = 128;
 
 size_t jit_min_tiles(int e) { return jitw_rows(e) ? kJitwMinTiles : kJitMinTiles; }
 size_t decode_code_bytes(int k, int e, size_t blocks);
 // generated code pays for a block of `tiles` column tiles: enough tiles to
-// amortise its code (every tile's workgroup fetches all of it), or code so
-// small that fetching it per tile costs little: (16, 8, 32000), 16 tiles and
-// 10 KB of code per block, decodes in 3.38 + 0.08 ms emission per 16384
-// blocks against 3.72 threaded (profiles/r03_ab/k16s32k/)
-constexpr size_t kJitCodePerTile = 1024;
+// amortise its code (every tile's workgroup fetches all of it), or, below
+// that, code small enough per tile ((16, 8) has 10 KB per block; at 16 tiles
+// 3.31 + 0.08 ms emission against 3.72 threaded per 16384 blocks,
+// profiles/r03_ab/k16s32k/, r03_ab/autoshort/)
+constexpr size_t kJitCodePerTile = 6144;
 bool jit_pays(int k, int e, size_t tiles)
 {
     return tiles >= jit_min_tiles(e) || decode_code_bytes(k, e, 1) <= kJitCodePerTile * tiles;

@@ -494,15 +494,17 @@ def test_auto_decode_kernel_by_batch_work(ctx, blocks, name):
     assert name in names and names[-1] == name, names
 
 
-@pytest.mark.parametrize("k,e,name", [(16, 8, "k_rs_jit(decode)"), (64, 16, "k_rs_tc(decode)"),
-                                      (64, 32, "k_rs_jit16(decode)")])
-def test_auto_decode_short_rows_by_code_size(ctx, k, e, name):
-    """Short rows (32000 bytes, 16 column tiles per block; README.rst:130-133
-    sweeps symbol_size 32000): AUTO takes generated code where a block's code
-    is small per tile ((16, 8): 10 KB) or the two-wave layout pays ((64, 32)),
-    threaded code where 80 KB of 8-row code would be fetched by each of 16
-    tiles ((64, 16)); erased rows poisoned."""
-    L, B = 32000, 256
+@pytest.mark.parametrize("k,e,L,B,name", [(16, 8, 32000, 256, "k_rs_jit(decode)"),
+                                          (128, 16, 32000, 256, "k_rs_jit(decode)"),
+                                          (64, 32, 32000, 256, "k_rs_jit16(decode)"),
+                                          (16, 8, 8192, 1024, "k_rs_jit(decode)"),
+                                          (128, 16, 8192, 1024, "k_rs_tc(decode)")])
+def test_auto_decode_short_rows_by_code_size(ctx, k, e, L, B, name):
+    """Short rows (README.rst:130-133 sweeps symbol_size 32000: 16 column
+    tiles per block): AUTO takes generated code from 16 tiles per block, and
+    below that where a block's code is at most 6 KB per tile ((16, 8) at 4
+    tiles: 10 KB per block), threaded code where (128, 16)'s 162 KB would be
+    fetched by each of 4 tiles; erased rows poisoned."""
     ctx.set_decode_kernel("auto")
     enc = rsgpu.GpuEncoder(k, L, e, blocks=B, seed=31, ctx=ctx)
     enc.encode_all()
