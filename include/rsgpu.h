@@ -153,7 +153,7 @@ size_t rsgpu_decode_workspace_bytes(int k, int e, size_t blocks);
  * the same bytes):
  *   AUTO        GENERATED when a block has >= 16 column tiles of 2 KB
  *               (len > 30 KiB), or fewer whose generated code is at most
- *               6 KB per tile, and the call has >= 4096 (block, tile)
+ *               2 KB per tile, and the call has >= 4096 (block, tile)
  *               pairs, else ONE_MATRIX (the default)
  *   ONE_MATRIX  closed-form e x k decode rows V_E^-1 [V_kept | I] (e <= 32),
  *               one threaded-code pass over the k - e survivors + e parity;

@@ -1015,10 +1015,11 @@ size_t jit_min_tiles(int e) { return jitw_rows(e) ? kJitwMinTiles : kJitMinTiles
 size_t decode_code_bytes(int k, int e, size_t blocks);
 // generated code pays for a block of `tiles` column tiles: enough tiles to
 // amortise its code (every tile's workgroup fetches all of it), or, below
-// that, code small enough per tile ((16, 8) has 10 KB per block; at 16 tiles
-// 3.31 + 0.08 ms emission against 3.72 threaded per 16384 blocks,
-// profiles/r03_ab/k16s32k/, r03_ab/autoshort/)
-constexpr size_t kJitCodePerTile = 6144;
+// that, code small enough per tile.  (16, 8) has 10 KB per block: at 8 tiles
+// (1.25 KB per tile) 3.46 + 0.15 ms emission against 3.84 threaded, at 4
+// tiles (2.5 KB) 3.71 + 0.29 against 3.90, per 16 GB of sources
+// (profiles/r03_ab/fewtiles/)
+constexpr size_t kJitCodePerTile = 2048;
 bool jit_pays(int k, int e, size_t tiles)
 {
     return tiles >= jit_min_tiles(e) || decode_code_bytes(k, e, 1) <= kJitCodePerTile * tiles;

@@ -497,14 +497,15 @@ def test_auto_decode_kernel_by_batch_work(ctx, blocks, name):
 @pytest.mark.parametrize("k,e,L,B,name", [(16, 8, 32000, 256, "k_rs_jit(decode)"),
                                           (128, 16, 32000, 256, "k_rs_jit(decode)"),
                                           (64, 32, 32000, 256, "k_rs_jit16(decode)"),
-                                          (16, 8, 8192, 1024, "k_rs_jit(decode)"),
-                                          (128, 16, 8192, 1024, "k_rs_tc(decode)")])
+                                          (16, 8, 16000, 512, "k_rs_jit(decode)"),
+                                          (16, 8, 8192, 1024, "k_rs_tc(decode)"),
+                                          (128, 16, 16000, 512, "k_rs_tc(decode)")])
 def test_auto_decode_short_rows_by_code_size(ctx, k, e, L, B, name):
     """Short rows (README.rst:130-133 sweeps symbol_size 32000: 16 column
     tiles per block): AUTO takes generated code from 16 tiles per block, and
-    below that where a block's code is at most 6 KB per tile ((16, 8) at 4
-    tiles: 10 KB per block), threaded code where (128, 16)'s 162 KB would be
-    fetched by each of 4 tiles; erased rows poisoned."""
+    below that where a block's code is at most 2 KB per tile ((16, 8), 10 KB
+    per block, at 8 tiles), threaded code above ((16, 8) at 4 tiles, (128,
+    16)'s 162 KB at 8); erased rows poisoned."""
     ctx.set_decode_kernel("auto")
     enc = rsgpu.GpuEncoder(k, L, e, blocks=B, seed=31, ctx=ctx)
     enc.encode_all()
