@@ -174,7 +174,10 @@ size_t rsgpu_decode_workspace_bytes(int k, int e, size_t blocks);
  * unaligned rows) or ONE_MATRIX. */
 #define RSGPU_DECODE_AUTO 0
 #define RSGPU_DECODE_ONE_MATRIX 1
-/* 2 is retired (a fused syndrome + solve kernel, never faster; removed) */
+/* Deprecated alias: 2 selected a fused syndrome + solve kernel (removed in
+ * round 3, never faster).  It is still accepted and runs ONE_MATRIX, which
+ * writes the same bytes. */
+#define RSGPU_DECODE_FUSED 2
 #define RSGPU_DECODE_GENERAL 3
 #define RSGPU_DECODE_GENERATED 4
 int rsgpu_set_decode_kernel(rsgpu_ctx *ctx, int kernel);

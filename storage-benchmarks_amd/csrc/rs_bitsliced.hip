@@ -39,11 +39,14 @@
 #include <utility>
 
 #include "bitslice.h"
+#include "diag_clock.h"
 #include "gf256.h"
 #include "rs_kernels.h"
 
 namespace rsgpu {
 namespace bs {
+
+RSGPU_DIAG_TABLE
 
 template <int K, int E, int C>
 struct PlanHolder {  // the code (K, E) and its Horner chunk C
@@ -336,10 +339,12 @@ template <int K, int E, int C, int NW>
 __global__ __launch_bounds__(64 * NW, (bs_waves_per_simd<E, NW>())) void k_rs_bs(Args a)
 {
     __shared__ uint4 lds[2][S * 2 * 64];
+    RSGPU_DIAG_BEGIN()
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     [&]<int... Gs>(std::integer_sequence<int, Gs...>) {
         ((wave == Gs ? run_group<K, E, C, NW, Gs>(a, lds) : void()), ...);
     }(std::make_integer_sequence<int, NW>{});
+    RSGPU_DIAG_END();
 }
 
 // Small batches of a single-chunk code (C == K, E <= 8; C2: one block of
@@ -427,14 +432,19 @@ hipError_t launch(const uint8_t* src, uint8_t* out, long long pitch, long long l
                   long long blocks, hipStream_t st)
 {
     // short rows whose last tile is partial: tiles over the rows of all
-    // blocks end to end (tile_pos)
-    const bool flat = blocks > 1 && len % 2048 != 0 && len < 65536 && pitch % 32 == 0;
+    // blocks end to end (tile_pos).  A lane addresses its rows from the
+    // tile's first block with a 32-bit offset (glds32's voffset): db * K *
+    // pitch + o, db <= 2048 / len + 1, must stay below 2^32
+    const bool flat = blocks > 1 && len % 2048 != 0 && len < 65536 && pitch % 32 == 0 &&
+                      (unsigned long long)(2048 / len + 2) * K * (unsigned long long)pitch < (1ull << 32);
     Args a{src, out, pitch, len, blocks, flat ? 1 : 0};
     dim3 grid(flat ? (unsigned)((blocks * len + 2047) / 2048) : (unsigned)((len + 2047) / 2048),
               flat ? 1u : (unsigned)blocks);
     hipLaunchKernelGGL((k_rs_bs<K, E, C, NW>), grid, dim3(64 * NW), 0, st, a);
     return hipGetLastError();
 }
+
+RSGPU_DIAG_READER(diag_read_bs)
 
 }  // namespace bs
 

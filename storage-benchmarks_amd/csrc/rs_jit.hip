@@ -23,6 +23,7 @@
 #include <utility>
 
 #include "bitslice.h"
+#include "diag_clock.h"
 #include "rs_jit.h"
 #include "rs_kernels.h"
 #include "tc_handlers.inc"
@@ -39,6 +40,8 @@ using bs::vconst;
 using bs::wait_vm;
 
 constexpr int C = 8;  // sources per LDS chunk (double-buffered)
+
+RSGPU_DIAG_TABLE
 
 // Instrumentation points of k_rs_jit.  The product instantiates JitHooks:
 // no timers, every wave runs its own block's code, wave 0 invalidates the
@@ -265,6 +268,7 @@ __global__ __launch_bounds__(64 * NV * TPW) __attribute__((amdgpu_num_vgpr(40)))
 {
     constexpr int CS = W::CS, R = W::R;
     __shared__ uint4 lds[2][TPW][CS * 2 * 64];
+    RSGPU_DIAG_BEGIN()
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int wave = wv % NV, tw = wv / NV;  // rows of the wave, its tile in the workgroup
     const int lane = threadIdx.x & 63;
@@ -396,6 +400,7 @@ __global__ __launch_bounds__(64 * NV * TPW) __attribute__((amdgpu_num_vgpr(40)))
                 ...);
         }(std::make_integer_sequence<int, R>{});
     }
+    RSGPU_DIAG_END();
 }
 
 // every 8-byte slot a return: a call that lands in code never written
@@ -407,6 +412,8 @@ __global__ void k_jit_fill(uint64_t* code, long long n)
          i += (long long)gridDim.x * blockDim.x)
         code[i] = ret;
 }
+
+RSGPU_DIAG_READER(diag_read_jitw)
 
 }  // namespace jitk
 

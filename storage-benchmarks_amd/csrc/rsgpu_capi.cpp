@@ -979,9 +979,10 @@ int rsgpu_set_encode_kernel(rsgpu_ctx* ctx, int kernel)
 
 int rsgpu_set_decode_kernel(rsgpu_ctx* ctx, int kernel)
 {
-    if (!ctx || kernel < RSGPU_DECODE_AUTO || kernel > RSGPU_DECODE_GENERATED || kernel == 2)
+    if (!ctx || kernel < RSGPU_DECODE_AUTO || kernel > RSGPU_DECODE_GENERATED)
         return fail(ctx, RSGPU_ERR_ARG, "rsgpu_set_decode_kernel: unknown kernel");
-    ctx->decode_kernel = kernel;
+    // the retired FUSED choice runs ONE_MATRIX (the same bytes; rsgpu.h)
+    ctx->decode_kernel = kernel == RSGPU_DECODE_FUSED ? RSGPU_DECODE_ONE_MATRIX : kernel;
     return RSGPU_OK;
 }
 
@@ -1009,6 +1010,9 @@ enum class Plan {
 // kJitXcdTiles the 8-row decode runs in XCD-contiguous order
 constexpr size_t kJitMinTiles = 16;
 constexpr size_t kJitwMinTiles = 16;
+// the general (k x k) decode through generated code in passes of 32 rows:
+// no A/B below 48 tiles was made for it (round 2's threshold stays)
+constexpr size_t kGeneralJitMinTiles = 48;
 constexpr size_t kJitXcdTiles = 128;
 
 size_t jit_min_tiles(int e) { return jitw_rows(e) ? kJitwMinTiles : kJitMinTiles; }
@@ -1040,7 +1044,7 @@ bool rows_aligned(size_t len, size_t pitch, const void* a, const void* b, const 
 // are long enough to amortise it (as decode_plan's AUTO), threaded code else
 Plan general_plan(rsgpu_ctx* ctx, size_t len)
 {
-    if ((len + 2047) / 2048 >= kJitMinTiles && ctx->decode_kernel != RSGPU_DECODE_ONE_MATRIX &&
+    if ((len + 2047) / 2048 >= kGeneralJitMinTiles && ctx->decode_kernel != RSGPU_DECODE_ONE_MATRIX &&
         jit_probe(ctx) == 1)
         return Plan::general_jit;
     return Plan::general_tc;
@@ -1382,6 +1386,12 @@ int rsgpu_decode_blocks(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch, 
                         const unsigned char* d_err, unsigned char* d_out, void* d_workspace,
                         int* d_status)
 {
+    // argument checks before any plan is made (decode_plan reads the context)
+    int rc = check_geom(ctx, k, e, len, pitch, blocks);
+    if (rc)
+        return rc;
+    if (e > 0 && (e > k || !d_err || !d_status))
+        return fail(ctx, RSGPU_ERR_ARG, "rsgpu_decode_blocks: bad arguments");
     if (blocks > kMaxGridBlocks) {
         // slices in stream order, each through the start of the workspace
         // (a slice's layout is no larger than the whole batch's)
@@ -1401,11 +1411,6 @@ int rsgpu_decode_blocks(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch, 
     if (e > 0 && e <= 8 && k <= 64 && len > 0 && blocks > 0 &&
         decode_plan(ctx, k, e, len, pitch, blocks, d_src, d_parity, d_out) == Plan::one_matrix &&
         (long long)((len + 2047) / 2048 * blocks) < kTcSplitMaxWork) {
-        int rc = check_geom(ctx, k, e, len, pitch, blocks);
-        if (rc)
-            return rc;
-        if (!d_err || !d_status)
-            return fail(ctx, RSGPU_ERR_ARG, "rsgpu_decode_blocks: bad arguments");
         TcFusedArgs f{};
         f.k = k;
         f.e = e;
@@ -1425,8 +1430,8 @@ int rsgpu_decode_blocks(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch, 
         RS_HIP(ctx, launch_rs_tc_fused(f, ctx->stream));
         return RSGPU_OK;
     }
-    int rc = rsgpu_decode_prepare(ctx, k, e, len, pitch, blocks, d_src, d_parity, d_err, d_out,
-                                  d_workspace, d_status);
+    rc = rsgpu_decode_prepare(ctx, k, e, len, pitch, blocks, d_src, d_parity, d_err, d_out,
+                              d_workspace, d_status);
     if (rc)
         return rc;
     return rsgpu_decode_apply(ctx, k, e, len, pitch, blocks, d_src, d_parity, d_out, d_workspace,

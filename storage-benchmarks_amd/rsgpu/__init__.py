@@ -39,14 +39,17 @@ __all__ = [
 ]
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "librsgpu.so")
+# RSGPU_LIB: another build of the same ABI (tools/bound_probe.py loads the
+# diagnostic build, tools/diag/librsgpu_diag.so); the product is librsgpu.so
+LIB_PATH = os.environ.get("RSGPU_LIB") or os.path.join(HERE, "librsgpu.so")
 
 RSGPU_OK = 0
 ERRORS = {-1: "RSGPU_ERR_ARG", -2: "RSGPU_ERR_HIP", -3: "RSGPU_ERR_SINGULAR",
           -4: "RSGPU_ERR_NOMEM", -5: "RSGPU_ERR_UNSUPPORTED"}
 MAX_SOURCES = 250  # TEST_SOURCES, isa.cpp:25-27
 # rsgpu_set_decode_kernel choices (include/rsgpu.h)
-DECODE_KERNELS = {"auto": 0, "one_matrix": 1, "general": 3, "generated": 4}
+DECODE_KERNELS = {"auto": 0, "one_matrix": 1, "general": 3, "generated": 4,
+                  "fused": 2}  # deprecated alias of one_matrix (rsgpu.h RSGPU_DECODE_FUSED)
 # rsgpu_set_encode_kernel choices (include/rsgpu.h)
 ENCODE_KERNELS = {"auto": 0, "compiled": 1, "generated": 2, "threaded": 3}
 

@@ -34,11 +34,11 @@ def orc():
     return Oracle()
 
 
-def encode_and_check(ctx, orc, k, e, L, B, coef=None, seed=5):
+def encode_and_check(ctx, orc, k, e, L, B, coef=None, seed=5, pitch=None):
     """encode_blocks over B synthetic blocks; parity of every block against
     the oracle with the same matrix."""
     dev = torch.device("cuda", 0)
-    pitch = (L + 255) // 256 * 256
+    pitch = pitch or (L + 255) // 256 * 256
     src = torch.empty(B * k * pitch, dtype=torch.uint8, device=dev)
     par = torch.full((B * e * pitch,), 0x5A, dtype=torch.uint8, device=dev)
     ctx.fill_synthetic(src, B * k, L, pitch, seed, 0)
@@ -123,6 +123,20 @@ def test_compiled_encode_short_rows_flat(ctx, orc, k, e, L, B):
         ctx.encode_blocks(k, e, L, pitch, B, src, par)
         torch.cuda.synchronize()
         assert (par.view(B, e, pitch)[:, :, L:] == 0x5A).all()
+    finally:
+        ctx.set_encode_kernel("auto")
+
+
+@pytest.mark.parametrize("k,e,L,B,pitch", [(64, 32, 32, 67, 1 << 20), (16, 4, 96, 130, 1 << 22)], ids=str)
+def test_compiled_encode_short_rows_wide_pitch(ctx, orc, k, e, L, B, pitch):
+    """Short rows in a widely pitched buffer: a flat tile's lanes address
+    their rows from the tile's first block with a 32-bit offset, which at
+    L = 32, pitch 1 MiB reaches 64 blocks x 64 rows x 1 MiB = 4 GiB -- the
+    launch keeps such geometries on per-block tiles,
+    and every block's parity equals the oracle's."""
+    ctx.set_encode_kernel("compiled")
+    try:
+        encode_and_check(ctx, orc, k, e, L, B, pitch=pitch)
     finally:
         ctx.set_encode_kernel("auto")
 
