@@ -72,14 +72,6 @@ def parse(argv=None):
                    choices=["auto", "generated", "one_matrix", "general"])
     p.add_argument("--encode-kernel", default="auto",
                    choices=["auto", "compiled", "generated", "threaded"])
-    p.add_argument("--jitw-tiles", type=int, default=0, help=argparse.SUPPRESS)  # A/B hook
-    p.add_argument("--jitw-prefetch", type=int, default=-1, help=argparse.SUPPRESS)  # A/B hook
-    # diagnostic: c4 batches from the third on keep the sources of two batches
-    # before (verification still checks every batch against its buffer)
-    p.add_argument("--no-regen", action="store_true", help=argparse.SUPPRESS)
-    # diagnostic: c4 generation of batch i+1 beside the verification of batch i
-    # (round-3 order) instead of after it
-    p.add_argument("--overlap-gen", action="store_true", help=argparse.SUPPRESS)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-threads", type=int, default=None)
     p.add_argument("--no-ref-base", action="store_true",
@@ -525,9 +517,9 @@ def run_streamed(args, rsgpu, ctx, dev, rank, world, k, e, L, total_blocks):
     setup() fills the blocks, encode_all, decode_all, verify_data): batch
     i+1's generation waits for batch i's verification, and the timed kernels
     run alone.  (Generating batch i+1 beside batch i's verification, the
-    round-3 order kept behind --overlap-gen, shortens the wall time but left
-    the encode that follows a verification 1.0-1.4 ms slower per batch,
-    profiles/r03_ab/verify/.)  Returns (timed seconds, wall seconds,
+    round-3 order, shortens the wall time but left the encode that follows a
+    verification 1.0-1.4 ms slower per batch, profiles/r03_ab/verify/.)
+    Returns (timed seconds, wall seconds,
     mismatching bytes, batches, kernel records)."""
     import numpy as np
     import torch
@@ -560,13 +552,12 @@ def run_streamed(args, rsgpu, ctx, dev, rank, world, k, e, L, total_blocks):
         h_err[i & 1][:nb] = torch.from_numpy(rsgpu.erasure_patterns(args.seed, b0, nb, k, e))
         with torch.cuda.stream(s_gen):
             if i >= 1:
-                # after batch i-1's verification (--overlap-gen: its decode);
-                # never beside the timed encode / decode kernels
-                s_gen.wait_event(ev_t[i - 1][1] if args.overlap_gen else ev_done[i - 1])
+                # after batch i-1's verification: never beside the timed
+                # encode / decode kernels
+                s_gen.wait_event(ev_done[i - 1])
             if i >= 2:
                 s_gen.wait_event(ev_done[i - 2])  # batch i-2 (same buffers) verified
-            if i < 2 or not args.no_regen:
-                gen_ctx.fill_synthetic(enc.src, nb * k, L, enc.pitch, args.seed, b0 * k)
+            gen_ctx.fill_synthetic(enc.src, nb * k, L, enc.pitch, args.seed, b0 * k)
             dec.err.view(-1)[:nb * e].copy_(h_err[i & 1][:nb].reshape(-1), non_blocking=True)
             ev_gen[i].record(s_gen)
 
@@ -587,8 +578,6 @@ def run_streamed(args, rsgpu, ctx, dev, rank, world, k, e, L, total_blocks):
         ctx.decode_blocks(k, e, L, enc.pitch, nb, enc.src, enc.par, dec.err, dec.out, dec.ws,
                           dec.status)
         ev_t[i][1].record(s_cmp)
-        if i + 1 < nb_total and args.overlap_gen:
-            generate(i + 1)
         if not args.no_verify:
             ctx.verify_blocks(k, e, L, enc.pitch, nb, enc.src, dec.out, dec.err, dec.mism)
             # fold this batch's mismatches (and failed blocks) into its slot
@@ -597,7 +586,7 @@ def run_streamed(args, rsgpu, ctx, dev, rank, world, k, e, L, total_blocks):
                 mism[i:i + 1].copy_(bad.view(1))
                 dec.mism.zero_()
         ev_done[i].record(s_cmp)
-        if i + 1 < nb_total and not args.overlap_gen:
+        if i + 1 < nb_total:
             generate(i + 1)
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
@@ -647,16 +636,6 @@ def main(argv=None):
     ctx.set_torch_stream()
     ctx.set_decode_kernel(args.decode_kernel)
     ctx.set_encode_kernel(args.encode_kernel)
-    if args.jitw_tiles:
-        import ctypes
-        f = rsgpu.lib().rsgpu_internal_set_jitw_tiles
-        f.argtypes = [ctypes.c_void_p, ctypes.c_int]
-        assert f(ctx._h, args.jitw_tiles) == 0
-    if args.jitw_prefetch >= 0:
-        import ctypes
-        f = rsgpu.lib().rsgpu_internal_set_jitw_prefetch
-        f.argtypes = [ctypes.c_void_p, ctypes.c_int]
-        assert f(ctx._h, args.jitw_prefetch) == 0
     alg = alg_bytes(k, e, L)
     rank_info = None
 

@@ -568,6 +568,8 @@ int jitw_rows(int e)
     return e > 24 ? 16 : e > 20 ? 12 : e > 16 ? 10 : 0;
 }
 
+int jitw_cs(int e) { return jitw_rows(e) == 16 ? jit::J16::CS : jitw_rows(e) == 12 ? jit::J12::CS : jit::J10::CS; }
+
 size_t jitw_chunk_stride(int e)
 {
     const int r = jitw_rows(e);

@@ -120,6 +120,8 @@ hipError_t launch_rs_jit(const JitArgs& a, long long blocks, hipStream_t st);
 // layout); code of
 // block b, wave w, chunk ch at code + ((b 2 + w) nch + ch) jitw_chunk_stride(e)
 int jitw_rows(int e);
+// sources per chunk of that layout (rs_jit.h Wide<R, CS>)
+int jitw_cs(int e);
 size_t jitw_chunk_stride(int e);
 size_t jitw_code_bytes(int k, int e, long long blocks);
 hipError_t launch_jitw_emit(int k, int e, long long blocks, const uint8_t* coef, const int* status,

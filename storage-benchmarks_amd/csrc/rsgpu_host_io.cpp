@@ -58,7 +58,9 @@ int io_setup(rsgpu_ctx* ctx, size_t bytes)
     if (!ctx->io_out)
         RS_HIP(ctx, hipStreamCreateWithFlags(&ctx->io_out, hipStreamNonBlocking));
     if (ctx->io_bytes < bytes) {
-        if (ctx->d_io) {
+        if (ctx->d_io) {  // no copy or kernel of an earlier call may still use it
+            RS_HIP(ctx, hipStreamSynchronize(ctx->io_in));
+            RS_HIP(ctx, hipStreamSynchronize(ctx->io_out));
             RS_HIP(ctx, hipStreamSynchronize(ctx->stream));
             RS_HIP(ctx, hipFree(ctx->d_io));
             ctx->d_io = nullptr;
@@ -93,6 +95,17 @@ int finish_io(rsgpu_ctx* ctx)
     RS_HIP(ctx, hipStreamSynchronize(ctx->stream));
     RS_HIP(ctx, hipStreamSynchronize(ctx->io_in));
     return RSGPU_OK;
+}
+
+// Runs the pipeline body, then drains all three streams whatever it
+// returned: no copy queued by the body may still move bytes into the
+// caller's host buffers (or out of the staging) after the call returns.
+template <class F>
+int with_drain(rsgpu_ctx* ctx, F&& body)
+{
+    const int rc = body();
+    const int rc2 = finish_io(ctx);
+    return rc ? rc : rc2;
 }
 
 }  // namespace
@@ -133,6 +146,7 @@ int rsgpu_encode_blocks_host(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pi
     if (rc)
         return rc;
     const size_t nch = (blocks + nb - 1) / nb;
+    return with_drain(ctx, [&]() -> int {
     for (size_t i = 0; i < nch; ++i) {
         const int s = (int)(i % kSlots);
         const size_t b0 = i * nb, n = std::min(nb, blocks - b0);
@@ -147,18 +161,17 @@ int rsgpu_encode_blocks_host(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pi
         RS_HIP(ctx, hipStreamWaitEvent(ctx->stream, ev_in, 0));
         if (i >= kSlots)  // its parity rows were copied out
             RS_HIP(ctx, hipStreamWaitEvent(ctx->stream, ev_out, 0));
-        rc = rsgpu_encode_blocks(ctx, k, e, len, pd, n, d_src, d_par, coef);
-        if (rc) {
-            (void)finish_io(ctx);
-            return rc;
-        }
+        const int rk = rsgpu_encode_blocks(ctx, k, e, len, pd, n, d_src, d_par, coef);
+        if (rk)
+            return rk;
         RS_HIP(ctx, hipEventRecord(ev_cmp, ctx->stream));
         RS_HIP(ctx, hipStreamWaitEvent(ctx->io_out, ev_cmp, 0));
         RS_HIP(ctx, copy_rows(h_parity + b0 * e * pitch, pitch, d_par, pd, len, n * e, hipMemcpyDeviceToHost,
                               ctx->io_out));
         RS_HIP(ctx, hipEventRecord(ev_out, ctx->io_out));
     }
-    return finish_io(ctx);
+    return RSGPU_OK;
+    });
 }
 
 int rsgpu_decode_blocks_host(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch, size_t blocks,
@@ -188,10 +201,11 @@ int rsgpu_decode_blocks_host(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pi
         return rc;
     unsigned char* d_err = (unsigned char*)ctx->d_io + err_off;
     int* d_status = (int*)((unsigned char*)ctx->d_io + st_off);
-    RS_HIP(ctx, hipMemcpyAsync(d_err, h_err, blocks * e, hipMemcpyHostToDevice, ctx->io_in));
     const bool runs = len >= kRunMinBytes;
     std::vector<char> erased(k);
     const size_t nch = (blocks + nb - 1) / nb;
+    rc = with_drain(ctx, [&]() -> int {
+    RS_HIP(ctx, hipMemcpyAsync(d_err, h_err, blocks * e, hipMemcpyHostToDevice, ctx->io_in));
     for (size_t i = 0; i < nch; ++i) {
         const int s = (int)(i % kSlots);
         const size_t b0 = i * nb, n = std::min(nb, blocks - b0);
@@ -233,18 +247,18 @@ int rsgpu_decode_blocks_host(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pi
         RS_HIP(ctx, hipStreamWaitEvent(ctx->stream, ev_in, 0));
         if (i >= kSlots)
             RS_HIP(ctx, hipStreamWaitEvent(ctx->stream, ev_out, 0));
-        rc = rsgpu_decode_blocks(ctx, k, e, len, pd, n, d_src, d_par, d_err + b0 * e, d_out, d_ws, d_status + b0);
-        if (rc) {
-            (void)finish_io(ctx);
-            return rc;
-        }
+        const int rk = rsgpu_decode_blocks(ctx, k, e, len, pd, n, d_src, d_par, d_err + b0 * e, d_out, d_ws,
+                                           d_status + b0);
+        if (rk)
+            return rk;
         RS_HIP(ctx, hipEventRecord(ev_cmp, ctx->stream));
         RS_HIP(ctx, hipStreamWaitEvent(ctx->io_out, ev_cmp, 0));
         RS_HIP(ctx, copy_rows(h_out + b0 * e * pitch, pitch, d_out, pd, len, n * e, hipMemcpyDeviceToHost,
                               ctx->io_out));
         RS_HIP(ctx, hipEventRecord(ev_out, ctx->io_out));
     }
-    rc = finish_io(ctx);
+    return RSGPU_OK;
+    });
     if (rc)
         return rc;
     if (h_status)

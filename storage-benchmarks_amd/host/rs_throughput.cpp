@@ -26,6 +26,7 @@
 #include <fstream>
 #include <memory>
 #include <mutex>
+#include <sstream>
 #include <string>
 #include <thread>
 #include <vector>
@@ -41,7 +42,7 @@ static void usage()
         "rs_throughput [--symbols N...] [--loss_rate R...] [--symbol_size P...]\n"
         "              [--type encoder|decoder...] [--runs N] [--blocks B]\n"
         "              [--seed S] [--device D] [--resident device|host]\n"
-        "              [--gpus N] [--same-device] [--csv_file F] [--json_file F]\n");
+        "              [--gpus N] [--same-device] [--csv_file F] [--json_file F] [--python_file F]\n");
 }
 
 // A reusable barrier for the per-GPU threads; a thread that fails breaks it
@@ -77,15 +78,34 @@ struct barrier {
     bool broken = false;
 };
 
-int main(int argc, char** argv)
+int main(int argc0, char** argv0)
 {
+    // boost::program_options syntax as the reference's README invokes it
+    // (README.rst:121, --symbols=100): "--opt=value" is "--opt value"
+    std::vector<std::string> toks;
+    for (int i = 0; i < argc0; ++i) {
+        const std::string t = argv0[i];
+        const size_t eq = t.find('=');
+        if (i > 0 && t.rfind("--", 0) == 0 && eq != std::string::npos) {
+            toks.push_back(t.substr(0, eq));
+            toks.push_back(t.substr(eq + 1));
+        } else {
+            toks.push_back(t);
+        }
+    }
+    std::vector<char*> av;
+    for (auto& t : toks)
+        av.push_back(t.data());
+    const int argc = (int)av.size();
+    char** argv = av.data();
+
     options o;
     uint32_t blocks = 1;
     uint64_t seed = 1;
     int device = 0, gpus = 1;
     bool same_device = false;
     resident where = resident::device;
-    std::string csv, json;
+    std::string csv, json, python;
     auto take = [&](int& i, auto fn) {
         while (i + 1 < argc && std::strncmp(argv[i + 1], "--", 2) != 0)
             fn(argv[++i]);
@@ -125,6 +145,8 @@ int main(int argc, char** argv)
             csv = argv[++i];
         } else if (a == "--json_file" && i + 1 < argc) {
             json = argv[++i];
+        } else if (a == "--python_file" && i + 1 < argc) {
+            python = argv[++i];
         } else {
             usage();
             return a == "--help" ? 0 : 2;
@@ -209,31 +231,59 @@ int main(int argc, char** argv)
                     row.bytes / row.seconds / 1073741824.0, row.seconds * 1e3);
         rows.push_back(row);
     }
+    // gauge's printers (README.rst:109-113): the same columns as a CSV table,
+    // a JSON document and a Python dictionary of columns
+    const std::vector<std::string> cols = {"testcase", "benchmark", "symbols", "symbol_size", "loss_rate",
+                                           "type", "erased_symbols", "blocks", "gpus", "resident",
+                                           "run", "seconds", "goodput"};
+    auto cells = [&](const result_row& r) {
+        auto num = [](double v) {
+            std::ostringstream o;
+            o << v;
+            return o.str();
+        };
+        return std::vector<std::pair<std::string, bool>>{  // (text, is a string)
+            {"MI355X", true}, {"ErasureCode", true}, {num(r.cs.symbols), false},
+            {num(r.cs.symbol_size), false}, {num(r.cs.loss_rate), false}, {r.cs.type, true},
+            {num(r.cs.erased_symbols), false}, {num(blocks), false}, {num(gpus), false},
+            {where == resident::host ? "host" : "device", true}, {num(r.run), false},
+            {num(r.seconds), false}, {num(r.goodput), false}};
+    };
     if (!csv.empty()) {
         std::ofstream f(csv);
-        f << "testcase,benchmark,symbols,symbol_size,loss_rate,type,erased_symbols,blocks,gpus,"
-             "resident,run,seconds,goodput\n";
-        for (const auto& r : rows)
-            f << "MI355X,ErasureCode," << r.cs.symbols << "," << r.cs.symbol_size << ","
-              << r.cs.loss_rate << "," << r.cs.type << "," << r.cs.erased_symbols << "," << blocks
-              << "," << gpus << "," << (where == resident::host ? "host" : "device") << "," << r.run
-              << "," << r.seconds << "," << r.goodput << "\n";
+        for (size_t c = 0; c < cols.size(); ++c)
+            f << cols[c] << (c + 1 < cols.size() ? "," : "\n");
+        for (const auto& r : rows) {
+            const auto v = cells(r);
+            for (size_t c = 0; c < v.size(); ++c)
+                f << v[c].first << (c + 1 < v.size() ? "," : "\n");
+        }
     }
     if (!json.empty()) {
         std::ofstream f(json);
         f << "[\n";
         for (size_t i = 0; i < rows.size(); ++i) {
-            const auto& r = rows[i];
-            f << "  {\"testcase\": \"MI355X\", \"benchmark\": \"ErasureCode\", \"symbols\": "
-              << r.cs.symbols << ", \"symbol_size\": " << r.cs.symbol_size
-              << ", \"loss_rate\": " << r.cs.loss_rate << ", \"type\": \"" << r.cs.type
-              << "\", \"erased_symbols\": " << r.cs.erased_symbols << ", \"blocks\": " << blocks
-              << ", \"gpus\": " << gpus << ", \"resident\": \""
-              << (where == resident::host ? "host" : "device") << "\", \"run\": " << r.run << ", \"seconds\": " << r.seconds
-              << ", \"goodput\": " << r.goodput << "}" << (i + 1 < rows.size() ? "," : "")
-              << "\n";
+            const auto v = cells(rows[i]);
+            f << "  {";
+            for (size_t c = 0; c < v.size(); ++c)
+                f << "\"" << cols[c] << "\": " << (v[c].second ? "\"" + v[c].first + "\"" : v[c].first)
+                  << (c + 1 < v.size() ? ", " : "");
+            f << "}" << (i + 1 < rows.size() ? "," : "") << "\n";
         }
         f << "]\n";
+    }
+    if (!python.empty()) {
+        std::ofstream f(python);
+        f << "{\n";
+        for (size_t c = 0; c < cols.size(); ++c) {
+            f << "    '" << cols[c] << "': [";
+            for (size_t i = 0; i < rows.size(); ++i) {
+                const auto v = cells(rows[i])[c];
+                f << (v.second ? "'" + v.first + "'" : v.first) << (i + 1 < rows.size() ? ", " : "");
+            }
+            f << "]" << (c + 1 < cols.size() ? "," : "") << "\n";
+        }
+        f << "}\n";
     }
     return rc;
 }

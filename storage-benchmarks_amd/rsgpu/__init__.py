@@ -129,6 +129,23 @@ def lib() -> C.CDLL:
     return _lib
 
 
+HOOKS_PATH = os.path.join(HERE, "librsgpu_testhooks.so")
+_hooks: Optional[C.CDLL] = None
+
+
+def testhooks() -> C.CDLL:
+    """The test / A-B hook library (rsgpu_testhooks.cpp), NOT the product:
+    host emitters of the generated code for the CPU suite, the device emitter
+    and the generated decode's layout knobs (rsgpu_internal_*).  librsgpu.so
+    itself exports only include/rsgpu.h."""
+    global _hooks
+    if _hooks is None:
+        if not os.path.exists(HOOKS_PATH):
+            raise RsGpuError(f"{HOOKS_PATH} is missing: build it with `make -C storage-benchmarks_amd`")
+        _hooks = C.CDLL(HOOKS_PATH)
+    return _hooks
+
+
 def _ptr(x) -> int:
     """Raw address of a torch tensor, numpy array or int."""
     if x is None:

@@ -38,6 +38,32 @@ def test_library_exports_every_header_symbol():
     assert rsgpu.EXPORTED_SYMBOLS == declared
 
 
+def test_library_exports_nothing_beyond_the_header():
+    """librsgpu.so's dynamic symbol table is exactly include/rsgpu.h (version
+    script csrc/rsgpu.map): no test hooks, no C++ internals."""
+    out = subprocess.run(["nm", "-D", "--defined-only", rsgpu.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    text = set(re.findall(r" [TWV] (\S+)", out))
+    assert text == set(header_symbols()), sorted(text ^ set(header_symbols()))
+
+
+def test_test_hooks_live_in_their_own_library():
+    out = subprocess.run(["nm", "-D", "--defined-only", rsgpu.HOOKS_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    hooks = set(re.findall(r" T (rsgpu_internal_\w+)", out))
+    assert {"rsgpu_internal_jit_emit", "rsgpu_internal_jitw_emit", "rsgpu_internal_jit_matrix_code",
+            "rsgpu_internal_jitw_matrix_code", "rsgpu_internal_jitw_emit_device",
+            "rsgpu_internal_set_jitw_tiles", "rsgpu_internal_set_jitw_prefetch"} <= hooks
+
+
+def test_decode_blocks_null_context_is_an_argument_error():
+    """rsgpu_decode_blocks checks its arguments before planning
+    (no device work: the call returns before touching the context)."""
+    L = rsgpu.lib()
+    assert L.rsgpu_decode_blocks(None, 16, 4, 1000000, 1000192, 1, None, None, None, None, None,
+                                 None) == -1
+
+
 def test_library_loads_and_binds():
     L = rsgpu.lib()
     assert L.rsgpu_version().decode().count(".") == 2

@@ -613,6 +613,36 @@ def test_cpp_runner_threads_share_a_gpu(tmp_path):
         assert f["gpus"] == "2" and f["resident"] == "device" and float(f["goodput"]) > 0
 
 
+def test_cpp_runner_printers_agree(tmp_path):
+    """gauge's three printers (README.rst:109-113) with the reference's own
+    invocation syntax (README.rst:121: --symbols=100 --symbol_size=1000000
+    --loss_rate=0.2 --python_file=... --csv_file=...): the Python file is a
+    dictionary of columns (ast.literal_eval), and it, the JSON document and
+    the CSV table hold the same rows."""
+    import ast
+    import csv
+    import json as js
+    runner = os.path.join(BIN, "rs_throughput")
+    py, cs, jn = tmp_path / "r.py", tmp_path / "r.csv", tmp_path / "r.json"
+    r = subprocess.run([runner, "--symbols=100", "--symbol_size=1000000", "--loss_rate=0.2", "--blocks=2",
+                        "--runs=2", f"--python_file={py}", f"--csv_file={cs}", f"--json_file={jn}"],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    cols = ast.literal_eval(py.read_text())
+    rows = list(csv.DictReader(open(cs)))
+    docs = js.loads(jn.read_text())
+    assert list(cols) == list(rows[0].keys()) == list(docs[0].keys())
+    assert len(rows) == len(docs) == 2 * 2  # encoder + decoder, 2 runs
+    for i, row in enumerate(rows):
+        for c, v in row.items():
+            if isinstance(cols[c][i], str):
+                assert cols[c][i] == v == docs[i][c], (c, i)
+            else:
+                assert float(cols[c][i]) == float(v) == float(docs[i][c]), (c, i)
+    assert set(cols["type"]) == {"encoder", "decoder"} and all(x == 100 for x in cols["symbols"])
+    assert all(x == 20 for x in cols["erased_symbols"]) and all(g > 0 for g in cols["goodput"])
+
+
 @pytest.mark.parametrize("extra", [[], ["--gpus", "2", "--same-device"]])
 def test_cpp_runner_host_resident(extra):
     """rs_throughput --resident host: the blocks live in pinned host memory as
@@ -707,7 +737,7 @@ def test_jitw_tiles_per_workgroup(ctx, tpw, k, e, L, B):
     rows poisoned, including tile counts that do not divide by the group
     (489, 16, 3, 7 tiles per block)."""
     import ctypes
-    f = rsgpu.lib().rsgpu_internal_set_jitw_tiles
+    f = rsgpu.testhooks().rsgpu_internal_set_jitw_tiles
     f.argtypes = [ctypes.c_void_p, ctypes.c_int]
     ctx.set_decode_kernel("generated")
     assert f(ctx._h, tpw) == 0
@@ -730,7 +760,7 @@ def test_jitw_code_prefetch(ctx, k, e, L, B):
     with the erased rows poisoned, for block-code sizes that leave some
     workgroups no line to fetch (one tile per block)."""
     import ctypes
-    f = rsgpu.lib().rsgpu_internal_set_jitw_prefetch
+    f = rsgpu.testhooks().rsgpu_internal_set_jitw_prefetch
     f.argtypes = [ctypes.c_void_p, ctypes.c_int]
     ctx.set_decode_kernel("generated")
     assert f(ctx._h, 1) == 0
@@ -759,7 +789,7 @@ def test_device_emitter_writes_the_host_emitters_code(ctx, k, e):
     coef[0, 1, :5] = 0          # zero coefficients: s_nop pairs
     coef[1, 0, :] = 1
     coef[2, :, 0] = 0x80
-    f = rsgpu.lib().rsgpu_internal_jitw_emit_device
+    f = rsgpu.testhooks().rsgpu_internal_jitw_emit_device
     f.restype = C.c_longlong
     f.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_size_t, C.c_void_p, C.c_void_p, C.c_size_t]
     need = f(ctx._h, k, e, blocks, coef.ctypes.data, None, 0)

@@ -32,7 +32,7 @@ CHUNK_STRIDE = 5056  # jit::chunk_stride(8): (16 + 8 * 624 + 8) rounded to 64
 
 def emit(k, e, coef):
     import rsgpu
-    f = rsgpu.lib().rsgpu_internal_jit_emit
+    f = rsgpu.testhooks().rsgpu_internal_jit_emit
     f.restype = C.c_longlong
     f.argtypes = [C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_size_t]
     coef = np.ascontiguousarray(coef, np.uint8)
@@ -158,7 +158,7 @@ def test_layout_independent_of_coefficients():
 
 def matrix_code(k, e, coef, max_ops=22):
     import rsgpu
-    f = rsgpu.lib().rsgpu_internal_jit_matrix_code
+    f = rsgpu.testhooks().rsgpu_internal_jit_matrix_code
     f.restype = C.c_longlong
     f.argtypes = [C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_size_t, C.POINTER(C.c_int), C.c_int]
     coef = np.ascontiguousarray(coef, np.uint8)
@@ -258,7 +258,7 @@ def wide_row0(e, w):
 
 def matrix_code_wide(k, e, coef, max_ops=22):
     import rsgpu
-    f = rsgpu.lib().rsgpu_internal_jitw_matrix_code
+    f = rsgpu.testhooks().rsgpu_internal_jitw_matrix_code
     f.restype = C.c_longlong
     f.argtypes = [C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_size_t, C.POINTER(C.c_int), C.c_int]
     coef = np.ascontiguousarray(coef, np.uint8)
@@ -334,7 +334,7 @@ def test_shared_matrix_code_wide(k, e, kind):
 
 def emitw(k, e, coef):
     import rsgpu
-    f = rsgpu.lib().rsgpu_internal_jitw_emit
+    f = rsgpu.testhooks().rsgpu_internal_jitw_emit
     f.restype = C.c_longlong
     f.argtypes = [C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_size_t]
     coef = np.ascontiguousarray(coef, np.uint8)

@@ -1,15 +1,54 @@
-"""Run bench.py against another build of librsgpu.so (same-box A/B of two
-library builds; tool, not product):
-    python3 tools/ab_lib.py LIB.so [bench.py arguments...]"""
+"""Same-box A/B harness around bench.py (a tool, not the product):
+
+    python3 tools/ab_lib.py [--lib LIB.so] [--jitw-tiles N] [--jitw-prefetch N] [bench.py args...]
+
+--lib           run bench.py against another build of librsgpu.so
+--jitw-tiles    column tiles per workgroup of the two-wave generated decode
+                (1, 2, 3; 0 = the library's choice)
+--jitw-prefetch its code prefetch into L2 (0 off, 1 on, -1 the library's choice)
+
+The knobs go through rsgpu_testhooks.cpp (librsgpu_testhooks.so), applied to
+every context bench.py creates; the product library exports none of them."""
+import argparse
+import ctypes
 import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "storage-benchmarks_amd"))
-import rsgpu  # noqa: E402
 
-rsgpu.LIB_PATH = os.path.abspath(sys.argv[1])
-import bench  # noqa: E402
 
-sys.exit(bench.main(sys.argv[2:]))
+def main() -> int:
+    ap = argparse.ArgumentParser(add_help=False)
+    ap.add_argument("--lib", default=None)
+    ap.add_argument("--jitw-tiles", type=int, default=None)
+    ap.add_argument("--jitw-prefetch", type=int, default=None)
+    ab, rest = ap.parse_known_args()
+    if ab.lib:
+        os.environ["RSGPU_LIB"] = os.path.abspath(ab.lib)
+    import rsgpu  # noqa: E402  (reads RSGPU_LIB)
+    if ab.lib:
+        rsgpu.LIB_PATH = os.path.abspath(ab.lib)
+    knobs = []
+    if ab.jitw_tiles is not None:
+        knobs.append(("rsgpu_internal_set_jitw_tiles", ab.jitw_tiles))
+    if ab.jitw_prefetch is not None:
+        knobs.append(("rsgpu_internal_set_jitw_prefetch", ab.jitw_prefetch))
+    if knobs:
+        init = rsgpu.Context.__init__
+
+        def patched(self, *a, **kw):
+            init(self, *a, **kw)
+            for name, v in knobs:
+                f = getattr(rsgpu.testhooks(), name)
+                f.argtypes = [ctypes.c_void_p, ctypes.c_int]
+                assert f(self._h, v) == 0, (name, v)
+
+        rsgpu.Context.__init__ = patched
+    import bench  # noqa: E402
+    return bench.main(rest)
+
+
+if __name__ == "__main__":
+    sys.exit(main())
