@@ -504,6 +504,7 @@ def alg_bytes(k, e, L):
             "k_rs_tc(encode)": blk_op, "k_rs_tc(decode)": blk_op, "k_rs_jit(decode)": blk_op,
             "k_rs_jit16(decode)": blk_op, "k_rs_jit10(decode)": blk_op, "k_rs_jit12(decode)": blk_op, "k_rs_jit(encode)": blk_op,
             "k_rs_jit16x4(decode)": blk_op, "k_rs_jit12x4(decode)": blk_op, "k_rs_jit10x4(decode)": blk_op,
+            "k_rs_jitw_passes(decode)": blk_op,
             "k_decode_prepare": 0.0, "k_decode_prepare_syn": 0.0}
 
 

@@ -215,6 +215,13 @@ RJ_HD inline bool code_word(const uint8_t* rows, int k, int nslot, int ch, int o
 // SIMD cover the LDS latency.
 RJ_HD constexpr int wide_waves(int e) { return e > 32 ? 4 : 2; }
 RJ_HD constexpr int wide_row0(int e, int w) { return w * e / wide_waves(e); }
+// e > 64 (k + e <= 250 allows e up to 125): passes of at most 64 rows, split
+// evenly (e = 100 as 50 + 50, e = 65 as 32 + 33), each pass one launch in the
+// layout of its own row count; pass p holds rows wide_pass_row0(e, p) ..
+// wide_pass_row0(e, p + 1) - 1.  A block's code is its passes' code in order.
+RJ_HD constexpr int wide_passes(int e) { return e > 64 ? (e + 63) / 64 : 1; }
+RJ_HD constexpr int wide_pass_row0(int e, int p) { return p * e / wide_passes(e); }
+RJ_HD constexpr int wide_pass_rows(int e, int p) { return wide_pass_row0(e, p + 1) - wide_pass_row0(e, p); }
 
 template <int R_, int CS_>
 struct Wide {

@@ -480,8 +480,12 @@ __constant__ jit::WideTables kWideTab = jit::wide_tables();
 // one 16-byte table load, two selects and ORs.  (Computing every word from
 // the coefficient's 8 x 8 matrix took ~3500 VALU + 2400 SALU per wave; the
 // emission of a C4 batch, 2.5 GB of code, 0.85-0.9 ms.)
+// e > 64: one launch per pass of the rows (rs_jit.h wide_passes), rows
+// row_base .. row_base + rows - 1 of the block's e decode rows, the pass's code
+// at pass_off in each block's block_stride bytes.
 template <class W>
-__global__ __launch_bounds__(256) void k_jitw_emit(int k, int e, const uint8_t* coef, const int* status,
+__global__ __launch_bounds__(256) void k_jitw_emit(int k, int e, int row_base, int rows, long long block_stride,
+                                                   long long pass_off, const uint8_t* coef, const int* status,
                                                    uint8_t* code)
 {
     constexpr int R = W::R, CS = W::CS, PW = W::PRE / 8;
@@ -491,9 +495,9 @@ __global__ __launch_bounds__(256) void k_jitw_emit(int k, int e, const uint8_t* 
     if (status[b] != 0)
         return;
     const int nch = (k + CS - 1) / CS;
-    const int r0 = jit::wide_row0(e, w), nslot = jit::wide_row0(e, w + 1) - r0;
+    const int r0 = row_base + jit::wide_row0(rows, w), nslot = jit::wide_row0(rows, w + 1) - jit::wide_row0(rows, w);
     const size_t stride = (size_t)W::chunk_stride();
-    uint8_t* cbase = code + ((size_t)b * jit::wide_waves(e) + w) * nch * stride;
+    uint8_t* cbase = code + (size_t)b * block_stride + pass_off + (size_t)w * nch * stride;
     const int sb = W::src_bytes(nslot);
     // every load of a phase in flight before its first use: the loops below
     // would otherwise wait a full memory latency per iteration
@@ -561,6 +565,7 @@ __global__ __launch_bounds__(256) void k_jitw_emit(int k, int e, const uint8_t* 
 }
 
 // rows per wave of the 2-wave layout for e rows, 0 = the 8-row layout
+// (e > 64: the layout of each pass, jitw_pass_rows)
 int jitw_rows(int e)
 {
     if (e > 32)  // four waves
@@ -576,27 +581,47 @@ size_t jitw_chunk_stride(int e)
     return r == 16 ? jit::J16::chunk_stride() : r == 12 ? jit::J12::chunk_stride() : jit::J10::chunk_stride();
 }
 
+// the layout covers e: 16 < e <= 64 in one launch, 64 < e <= 125 in passes
+bool jitw_layout(int e) { return e > 16 && (e <= 64 || (e <= 128 && jitw_rows(jit::wide_pass_rows(e, 0)) &&
+                                                        jitw_rows(jit::wide_pass_rows(e, jit::wide_passes(e) - 1)))); }
+
+// one block's code of a pass of `rows` (<= 64) rows
+size_t jitw_pass_bytes(int k, int rows)
+{
+    const int cs = jitw_cs(rows);
+    return (size_t)jit::wide_waves(rows) * ((k + cs - 1) / cs) * jitw_chunk_stride(rows);
+}
+
+size_t jitw_pass_offset(int k, int e, int p)
+{
+    size_t o = 0;
+    for (int q = 0; q < p; ++q)
+        o += jitw_pass_bytes(k, jit::wide_pass_rows(e, q));
+    return o;
+}
+
 size_t jitw_code_bytes(int k, int e, long long blocks)
 {
-    const int r = jitw_rows(e);
-    const int cs = r == 16 ? jit::J16::CS : r == 12 ? jit::J12::CS : jit::J10::CS;
-    return (size_t)blocks * jit::wide_waves(e) * ((k + cs - 1) / cs) * jitw_chunk_stride(e);
+    return (size_t)blocks * jitw_pass_offset(k, e, jit::wide_passes(e));
 }
 
 hipError_t launch_jitw_emit(int k, int e, long long blocks, const uint8_t* coef, const int* status,
                             uint8_t* code, hipStream_t st)
 {
-    if (k <= 0 || k > 250 || !jitw_rows(e) || k + e > 250 || blocks <= 0 || !coef || !status || !code)
+    if (k <= 0 || k > 250 || !jitw_layout(e) || k + e > 250 || blocks <= 0 || !coef || !status || !code)
         return hipErrorInvalidValue;
-    if (jitw_rows(e) == 16)
-        hipLaunchKernelGGL(k_jitw_emit<jit::J16>, dim3(jit::wide_waves(e), (unsigned)blocks), dim3(256), 0, st, k, e, coef, status,
-                           code);
-    else if (jitw_rows(e) == 12)
-        hipLaunchKernelGGL(k_jitw_emit<jit::J12>, dim3(jit::wide_waves(e), (unsigned)blocks), dim3(256), 0, st, k, e, coef, status,
-                           code);
-    else
-        hipLaunchKernelGGL(k_jitw_emit<jit::J10>, dim3(jit::wide_waves(e), (unsigned)blocks), dim3(256), 0, st, k, e, coef, status,
-                           code);
+    const long long bs = (long long)jitw_code_bytes(k, e, 1);
+    for (int p = 0; p < jit::wide_passes(e); ++p) {
+        const int r0 = jit::wide_pass_row0(e, p), rows = jit::wide_pass_rows(e, p);
+        const long long off = (long long)jitw_pass_offset(k, e, p);
+        const dim3 grid(jit::wide_waves(rows), (unsigned)blocks);
+        if (jitw_rows(rows) == 16)
+            hipLaunchKernelGGL(k_jitw_emit<jit::J16>, grid, dim3(256), 0, st, k, e, r0, rows, bs, off, coef, status, code);
+        else if (jitw_rows(rows) == 12)
+            hipLaunchKernelGGL(k_jitw_emit<jit::J12>, grid, dim3(256), 0, st, k, e, r0, rows, bs, off, coef, status, code);
+        else
+            hipLaunchKernelGGL(k_jitw_emit<jit::J10>, grid, dim3(256), 0, st, k, e, r0, rows, bs, off, coef, status, code);
+    }
     return hipGetLastError();
 }
 

@@ -124,6 +124,11 @@ int jitw_rows(int e);
 int jitw_cs(int e);
 size_t jitw_chunk_stride(int e);
 size_t jitw_code_bytes(int k, int e, long long blocks);
+// the wide layout covers e (16 < e <= 64 one launch; 64 < e <= 125 in passes
+// of <= 64 rows, rs_jit.h wide_passes), and a pass's place in a block's code
+bool jitw_layout(int e);
+size_t jitw_pass_bytes(int k, int rows);
+size_t jitw_pass_offset(int k, int e, int p);
 hipError_t launch_jitw_emit(int k, int e, long long blocks, const uint8_t* coef, const int* status,
                             uint8_t* code, hipStream_t st);
 hipError_t launch_rs_jitw(const JitArgs& a, long long blocks, hipStream_t st);

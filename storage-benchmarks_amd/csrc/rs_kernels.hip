@@ -912,11 +912,11 @@ __global__ __launch_bounds__(256) void k_decode_prepare_syn(int k, int e,
     const int tid = threadIdx.x, nt = blockDim.x;
     const uint8_t* eb = err + (size_t)b * e;
     uint8_t* lv = A + e * e;   // survivors, k - e bytes (256 reserved)
-    uint8_t* lam = lv + 256;   // Lambda coefficients, e + 1 (64 reserved)
-    uint8_t* lw = lam + 64;    // log w_i (64 reserved)
-    uint8_t* lb = lw + 64;     // log Lambda(b_q) (256 reserved)
-    uint8_t* ea = lb + 256;    // the erased originals j_i (64 reserved)
-    uint8_t* aa = ea + 64;     // a_i = 2^(j_i) (64 reserved)
+    uint8_t* lam = lv + 256;   // Lambda coefficients, e + 1 (128 reserved)
+    uint8_t* lw = lam + 128;   // log w_i (128 reserved)
+    uint8_t* lb = lw + 128;    // log Lambda(b_q) (256 reserved)
+    uint8_t* ea = lb + 256;    // the erased originals j_i (128 reserved)
+    uint8_t* aa = ea + 128;    // a_i = 2^(j_i) (128 reserved)
     for (int i = tid; i < 512; i += nt) {
         gexp[i] = kGfTables.exp[i];
         if (i < 256)
@@ -968,11 +968,27 @@ __global__ __launch_bounds__(256) void k_decode_prepare_syn(int k, int e,
             if (!er)
                 lv[j - below] = (uint8_t)j;
         }
-        if (tid < 64) {  // Lambda(z) by wave 0, lane m holding the coefficient of z^m
-            uint8_t lm = tid == 0 ? 1 : 0;  // e <= 32 < 64 lanes
-            for (int l = 0; l < e; ++l) {   // times (z + a_l): lam_m <- lam_{m-1} + a_l lam_m
-                const int below = __shfl_up((int)lm, 1);
-                lm = (uint8_t)(tid == 0 ? 0 : below) ^ gmul(aa[l], lm);
+        if (e < 64) {
+            if (tid < 64) {  // Lambda(z) by wave 0, lane m holding the coefficient of z^m
+                uint8_t lm = tid == 0 ? 1 : 0;  // e + 1 <= 64 lanes
+                for (int l = 0; l < e; ++l) {   // times (z + a_l): lam_m <- lam_{m-1} + a_l lam_m
+                    const int below = __shfl_up((int)lm, 1);
+                    lm = (uint8_t)(tid == 0 ? 0 : below) ^ gmul(aa[l], lm);
+                }
+                if (tid <= e)
+                    lam[tid] = lm;
+            }
+        } else {
+            // e + 1 > 64 coefficients (e <= 125): thread m <= e holds lam_m and
+            // the product grows through LDS, one factor per barrier pair
+            uint8_t lm = tid == 0 ? 1 : 0;
+            for (int l = 0; l < e; ++l) {
+                if (tid <= e)
+                    lam[tid] = lm;
+                __syncthreads();
+                if (tid <= e)
+                    lm = (uint8_t)(tid == 0 ? 0 : lam[tid - 1]) ^ gmul(aa[l], lm);
+                __syncthreads();
             }
             if (tid <= e)
                 lam[tid] = lm;
@@ -1038,7 +1054,7 @@ __global__ __launch_bounds__(256) void k_decode_prepare_syn(int k, int e,
     }
 }
 
-size_t decode_prepare_syn_lds_bytes(int e) { return 832 + (size_t)e * e + 256 + 512; }
+size_t decode_prepare_syn_lds_bytes(int e) { return 832 + (size_t)e * e + 1024; }
 
 hipError_t launch_decode_prepare_syn(int k, int e, long long blocks, const uint8_t* err,
                                      uint8_t* out, long long out_pitch, const uint8_t** srcs,
@@ -1046,7 +1062,7 @@ hipError_t launch_decode_prepare_syn(int k, int e, long long blocks, const uint8
                                      const uint8_t* src, const uint8_t* par,
                                      unsigned long long* dir_addr, uint8_t* jit_coef, hipStream_t st)
 {
-    if (k <= 0 || k > 250 || e <= 0 || e > (jit_coef ? 63 : 32) || k + e > 250 ||
+    if (k <= 0 || k > 250 || e <= 0 || e > (jit_coef ? 125 : 32) || e > k || k + e > 250 ||
         (!jit_coef && (!tc_table || !dir_addr)))
         return hipErrorInvalidValue;
     static bool attr_set = false;

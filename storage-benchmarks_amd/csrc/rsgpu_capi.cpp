@@ -995,7 +995,7 @@ constexpr size_t kJitwMinTiles = 16;
 constexpr size_t kGeneralJitMinTiles = 48;
 constexpr size_t kJitXcdTiles = 128;
 
-size_t jit_min_tiles(int e) { return jitw_rows(e) ? kJitwMinTiles : kJitMinTiles; }
+size_t jit_min_tiles(int e) { return jitw_layout(e) ? kJitwMinTiles : kJitMinTiles; }
 size_t decode_code_bytes(int k, int e, size_t blocks);
 // generated code pays for a block of `tiles` column tiles: enough tiles to
 // amortise its code (every tile's workgroup fetches all of it), or, below
@@ -1036,9 +1036,9 @@ Plan decode_plan(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch, size_t 
     if (!rows_aligned(len, pitch, src, par, out) || !tc_ready(ctx))
         return Plan::general_dot;
     const int want = ctx->decode_kernel;
-    // the closed-form rows need Lambda's e + 1 coefficients in one wave
-    // (e <= 63); the threaded-code kernel takes e <= 32
-    const bool gen_ok = e <= 63 && jit_probe(ctx) == 1 && want != RSGPU_DECODE_ONE_MATRIX &&
+    // the closed-form rows serve every e (Lambda's e + 1 coefficients in one
+    // wave up to e = 63, in LDS above); the threaded-code kernel takes e <= 32
+    const bool gen_ok = jit_probe(ctx) == 1 && want != RSGPU_DECODE_ONE_MATRIX &&
                         want != RSGPU_DECODE_GENERAL &&
                         (want == RSGPU_DECODE_GENERATED || jit_pays(k, e, (len + 2047) / 2048));
     if (e > 32 && gen_ok)
@@ -1090,7 +1090,7 @@ WsLayout ws_layout(int k, int e, size_t blocks)
 // XCD-contiguous order 3.7 % faster than the 8-row kernel.
 size_t decode_code_bytes(int k, int e, size_t blocks)
 {
-    return jitw_rows(e) ? jitw_code_bytes(k, e, (long long)blocks) : jit_code_bytes(k, e, (long long)blocks);
+    return jitw_layout(e) ? jitw_code_bytes(k, e, (long long)blocks) : jit_code_bytes(k, e, (long long)blocks);
 }
 
 // k_jit_emit / k_jitw_emit: the code of every block from its decode rows
@@ -1104,9 +1104,9 @@ int emit_decode_code(rsgpu_ctx* ctx, int k, int e, size_t blocks, const uint8_t*
     ctx->jit_key.blocks = blocks;
     ctx->jit_key.ws = ws;
     ctx->jit_key.gen = ++ctx->jit_gen;
-    if (jitw_rows(e)) {
-        KTimer ke(ctx, jitw_rows(e) == 16 ? "k_jit16_emit" : jitw_rows(e) == 12 ? "k_jit12_emit" : "k_jit10_emit",
-                  blocks);
+    if (jitw_layout(e)) {
+        const int r = jitw_rows(jit::wide_pass_rows(e, 0));
+        KTimer ke(ctx, r == 16 ? "k_jit16_emit" : r == 12 ? "k_jit12_emit" : "k_jit10_emit", blocks);
         RS_HIP(ctx, launch_jitw_emit(k, e, (long long)blocks, coef, d_status, (uint8_t*)ctx->d_jit, ctx->stream));
     } else {
         KTimer ke(ctx, "k_jit_emit", blocks);
@@ -1131,46 +1131,51 @@ int jit_decode_launch(rsgpu_ctx* ctx, int k, int e, size_t len, size_t blocks, c
         return fail(ctx, RSGPU_ERR_ARG,
                     "rsgpu_decode_apply: the generated code belongs to another prepare "
                     "(re-run rsgpu_decode_prepare for this workspace)");
-    if (jitw_rows(e)) {
-        JitArgs j{};
-        j.srcs = d_srcs;
-        j.dsts = d_dsts;
-        j.code = (const uint8_t*)ctx->d_jit;
-        j.chunk_stride = (long long)jitw_chunk_stride(e);
-        j.block_stride = (long long)jitw_code_bytes(k, e, 1);
-        j.k = k;
-        j.rows = e;
-        j.dst_stride = e;
-        j.len = (long long)len;
-        j.status = d_status;
-        // each XCD a contiguous range of (block, tile): a block's code is
-        // fetched into one L2, not eight -- 3.7 % faster at C3 for the
-        // 16-row kernel (23.3 vs 24.2 ms, profiles/r02_ab/jit_rows16/xcd_*.log),
-        // where the 8-row kernel measured 1 % slower
-        j.xcd_order = 1;
-        // two column tiles per workgroup: the waves with the same rows share
-        // their code's instruction-cache lines (C4 13.7 vs 14.2 ms per 16384
-        // blocks, C3 23.2-23.3 vs 23.4-23.5, C5 12.7-12.8 vs 12.8-12.9;
-        // three tiles: 20-30 % slower; profiles/r03_ab/tpw/)
-        j.tiles_per_wg = jit::wide_waves(e) == 4 ? 1 : ctx->jitw_tpw ? ctx->jitw_tpw : 2;
-        // short rows: the block's few workgroups pull its code into L2 before
-        // the instruction fetch misses on it line by line (C4: 12.8 vs 13.7
-        // ms per 16384 blocks; C3, 245 workgroups per block, unchanged:
-        // profiles/r03_ab/prefetch/)
-        {
-            const long long wgs = ((long long)((len + 2047) / 2048) + j.tiles_per_wg - 1) / j.tiles_per_wg;
-            const long long lines = (long long)jitw_code_bytes(k, e, 1) / 128;
-            j.code_prefetch = ctx->jitw_prefetch >= 0 ? ctx->jitw_prefetch : lines >= 32 * wgs;
+    if (jitw_layout(e)) {
+        // one launch per pass of <= 64 rows (one pass for e <= 64)
+        const size_t bs = jitw_code_bytes(k, e, 1);
+        for (int p = 0; p < jit::wide_passes(e); ++p) {
+            const int r0 = jit::wide_pass_row0(e, p), rows = jit::wide_pass_rows(e, p);
+            JitArgs j{};
+            j.srcs = d_srcs;
+            j.dsts = d_dsts + r0;
+            j.code = (const uint8_t*)ctx->d_jit + jitw_pass_offset(k, e, p);
+            j.chunk_stride = (long long)jitw_chunk_stride(rows);
+            j.block_stride = (long long)bs;
+            j.k = k;
+            j.rows = rows;
+            j.dst_stride = e;
+            j.len = (long long)len;
+            j.status = d_status;
+            // each XCD a contiguous range of (block, tile): a block's code is
+            // fetched into one L2, not eight -- 3.7 % faster at C3 for the
+            // 16-row kernel (23.3 vs 24.2 ms, profiles/r02_ab/jit_rows16/xcd_*.log),
+            // where the 8-row kernel measured 1 % slower
+            j.xcd_order = 1;
+            // two column tiles per workgroup: the waves with the same rows share
+            // their code's instruction-cache lines (C4 13.7 vs 14.2 ms per 16384
+            // blocks, C3 23.2-23.3 vs 23.4-23.5, C5 12.7-12.8 vs 12.8-12.9;
+            // three tiles: 20-30 % slower; profiles/r03_ab/tpw/)
+            j.tiles_per_wg = jit::wide_waves(rows) == 4 ? 1 : ctx->jitw_tpw ? ctx->jitw_tpw : 2;
+            // short rows: the block's few workgroups pull its code into L2 before
+            // the instruction fetch misses on it line by line (C4: 12.8 vs 13.7
+            // ms per 16384 blocks; C3, 245 workgroups per block, unchanged:
+            // profiles/r03_ab/prefetch/)
+            {
+                const long long wgs = ((long long)((len + 2047) / 2048) + j.tiles_per_wg - 1) / j.tiles_per_wg;
+                const long long lines = (long long)jitw_pass_bytes(k, rows) / 128;
+                j.code_prefetch = ctx->jitw_prefetch >= 0 ? ctx->jitw_prefetch : lines >= 32 * wgs;
+            }
+            const int r = jitw_rows(rows);
+            KTimer kt(ctx,
+                      e > 64  ? "k_rs_jitw_passes(decode)"
+                      : e > 32 ? (r == 16 ? "k_rs_jit16x4(decode)" : r == 12 ? "k_rs_jit12x4(decode)" : "k_rs_jit10x4(decode)")
+                      : r == 16 ? "k_rs_jit16(decode)"
+                      : r == 12 ? "k_rs_jit12(decode)"
+                                : "k_rs_jit10(decode)",
+                      blocks);
+            RS_HIP(ctx, launch_rs_jitw(j, (long long)blocks, ctx->stream));
         }
-        KTimer kt(ctx,
-                  e > 32 ? (jitw_rows(e) == 16   ? "k_rs_jit16x4(decode)"
-                            : jitw_rows(e) == 12 ? "k_rs_jit12x4(decode)"
-                                                 : "k_rs_jit10x4(decode)")
-                  : jitw_rows(e) == 16 ? "k_rs_jit16(decode)"
-                  : jitw_rows(e) == 12 ? "k_rs_jit12(decode)"
-                                       : "k_rs_jit10(decode)",
-                  blocks);
-        RS_HIP(ctx, launch_rs_jitw(j, (long long)blocks, ctx->stream));
         return RSGPU_OK;
     }
     const int nch = (k + 7) / 8, nwt = (e + 7) / 8;

@@ -26,20 +26,22 @@ namespace {
 
 constexpr size_t kMaxGridBlocks = 65535;
 
-// One block's code in the two-wave layout (rs_jit.h Wide<R, CS>) for the
-// e x k matrix coef, from Wide::code_word: wave w, chunk ch at
-// (w nch + ch) chunk_stride; unused words are returns.
+// One pass's code in the two- / four-wave layout (rs_jit.h Wide<R, CS>):
+// rows row_base .. row_base + rows - 1 of the e x k matrix coef, from
+// Wide::code_word: wave w, chunk ch at (w nch + ch) chunk_stride from o64;
+// unused words are returns.
 template <class W>
-void jitw_emit_host(int k, int e, const unsigned char* coef, uint64_t* o64)
+void jitw_emit_host(int k, int row_base, int rows, const unsigned char* coef, uint64_t* o64)
 {
     const int nch = (k + W::CS - 1) / W::CS, stride_w = W::chunk_stride() / 8;
-    for (int w = 0; w < jit::wide_waves(e); ++w) {
-        const int r0 = jit::wide_row0(e, w), nslot = jit::wide_row0(e, w + 1) - r0;
-        const unsigned char* rows = coef + (size_t)r0 * k;
+    for (int w = 0; w < jit::wide_waves(rows); ++w) {
+        const int r0 = row_base + jit::wide_row0(rows, w);
+        const int nslot = jit::wide_row0(rows, w + 1) - jit::wide_row0(rows, w);
+        const unsigned char* cr = coef + (size_t)r0 * k;
         for (int ch = 0; ch < nch; ++ch)
             for (int o = 0; o < stride_w; ++o) {
                 uint64_t word;
-                if (W::code_word(rows, k, nslot, ch, o, &word))
+                if (W::code_word(cr, k, nslot, ch, o, &word))
                     o64[((size_t)w * nch + ch) * stride_w + o] = word;
             }
     }
@@ -116,12 +118,13 @@ long long rsgpu_internal_jit_emit(int k, int e, const unsigned char* coef, unsig
 }
 
 // Test hook (not part of include/rsgpu.h): the same for the two- and
-// four-wave layouts of k_rs_jitw (rs_jit.h Wide, jitw_rows, wide_waves),
-// from Wide::code_word (the words k_jitw_emit writes).
+// four-wave layouts of k_rs_jitw (rs_jit.h Wide, jitw_rows, wide_waves; e >
+// 64 as passes of <= 64 rows, wide_passes), from Wide::code_word (the words
+// k_jitw_emit writes).
 long long rsgpu_internal_jitw_emit(int k, int e, const unsigned char* coef, unsigned char* out,
                                    size_t out_bytes)
 {
-    if (k <= 0 || !jitw_rows(e) || k + e > 250 || !coef)
+    if (k <= 0 || !jitw_layout(e) || k + e > 250 || !coef)
         return -1;
     const size_t need = jitw_code_bytes(k, e, 1);
     if (!out || out_bytes < need)
@@ -129,12 +132,16 @@ long long rsgpu_internal_jitw_emit(int k, int e, const unsigned char* coef, unsi
     uint64_t* o64 = reinterpret_cast<uint64_t*>(out);
     for (size_t i = 0; i < need / 8; ++i)
         o64[i] = (uint64_t)jit::S_NOP0 << 32 | jit::S_SETPC_82;
-    if (jitw_rows(e) == 16)
-        jitw_emit_host<jit::J16>(k, e, coef, o64);
-    else if (jitw_rows(e) == 12)
-        jitw_emit_host<jit::J12>(k, e, coef, o64);
-    else
-        jitw_emit_host<jit::J10>(k, e, coef, o64);
+    for (int p = 0; p < jit::wide_passes(e); ++p) {  // passes of <= 64 rows (e > 64)
+        const int r0 = jit::wide_pass_row0(e, p), rows = jit::wide_pass_rows(e, p);
+        uint64_t* po = o64 + jitw_pass_offset(k, e, p) / 8;
+        if (jitw_rows(rows) == 16)
+            jitw_emit_host<jit::J16>(k, r0, rows, coef, po);
+        else if (jitw_rows(rows) == 12)
+            jitw_emit_host<jit::J12>(k, r0, rows, coef, po);
+        else
+            jitw_emit_host<jit::J10>(k, r0, rows, coef, po);
+    }
     return (long long)need;
 }
 
@@ -162,7 +169,7 @@ long long rsgpu_internal_jitw_matrix_code(int k, int e, const unsigned char* coe
 long long rsgpu_internal_jitw_emit_device(rsgpu_ctx* ctx, int k, int e, size_t blocks,
                                           const unsigned char* coef, unsigned char* out, size_t out_bytes)
 {
-    if (!ctx || k <= 0 || !jitw_rows(e) || k + e > 250 || blocks == 0 || blocks > kMaxGridBlocks || !coef)
+    if (!ctx || k <= 0 || !jitw_layout(e) || k + e > 250 || blocks == 0 || blocks > kMaxGridBlocks || !coef)
         return -1;
     const size_t need = jitw_code_bytes(k, e, (long long)blocks);
     if (!out || out_bytes < need)

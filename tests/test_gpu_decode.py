@@ -94,7 +94,11 @@ GEOMS = [(16, 4, 1000000, 2), (64, 32, 1000000, 2), (100, 20, 1000000, 2), (16, 
          (50, 25, 98304, 3), (31, 31, 4096, 2), (218, 32, 2048, 2),
          (17, 17, 65536, 2), (64, 19, 4096, 3), (230, 20, 2048, 2),
          # 20 < e <= 24: 12 rows per wave (k_rs_jit12)
-         (48, 24, 65536, 2), (21, 21, 4096, 3), (226, 24, 2048, 2)]
+         (48, 24, 65536, 2), (21, 21, 4096, 3), (226, 24, 2048, 2),
+         # e > 64 (k + e <= 250 allows 125): closed-form rows through LDS,
+         # generated code in passes of <= 64 rows, four waves per tile
+         (150, 100, 65536, 2), (125, 125, 32768, 2), (160, 65, 65536, 2), (186, 64, 65536, 2),
+         (130, 120, 4096, 2)]
 
 
 @pytest.mark.parametrize("kernel", KERNELS)
@@ -775,7 +779,8 @@ def test_jitw_code_prefetch(ctx, k, e, L, B):
 
 
 @pytest.mark.parametrize("k,e", [(64, 32), (25, 25), (218, 32), (48, 24), (21, 21), (100, 20), (17, 17),
-                                 (230, 20), (100, 50), (128, 64), (70, 45), (40, 33)])
+                                 (230, 20), (100, 50), (128, 64), (70, 45), (40, 33),
+                                 (150, 100), (125, 125), (160, 65)])
 def test_device_emitter_writes_the_host_emitters_code(ctx, k, e):
     """k_jitw_emit (table-driven, on the device) writes, block for block and
     word for word, the code of the host emitter Wide::code_word, which the
@@ -801,3 +806,29 @@ def test_device_emitter_writes_the_host_emitters_code(ctx, k, e):
         host = emitw(k, e, coef[b])
         assert host.size == per
         assert np.array_equal(out[b * per:(b + 1) * per], host), b
+
+
+@pytest.mark.parametrize("k,e,L", [(150, 100, 1000000), (125, 125, 1000000), (186, 64, 1000000),
+                                   (160, 65, 65536)])
+def test_wide_rows_decode_in_at_most_two_launches(ctx, k, e, L):
+    """e > 64 (isa.cpp:25-27 allows k + e <= 250): the decode rows come in
+    closed form (no k x k inversion) and the generated code runs in passes of
+    <= 64 rows, four waves per tile, each source read and transposed once per
+    pass: at most two decode launches; the erased rows are poisoned."""
+    B = 2
+    enc = rsgpu.GpuEncoder(k, L, e, blocks=B, seed=5, ctx=ctx)
+    enc.encode_all()
+    dec = rsgpu.GpuDecoder(k, L, e, blocks=B, seed=5, ctx=ctx)
+    torch.cuda.synchronize()
+    ctx.timing_read()
+    ctx.timing_enable(True)
+    try:
+        assert decode_poisoned(ctx, enc, dec)
+        names = [r[0] for r in ctx.timing_read()]
+    finally:
+        ctx.timing_enable(False)
+    assert "k_decode_prepare" not in names, names
+    assert "k_decode_prepare_syn" in names
+    apply = [n for n in names if n.startswith("k_rs_jit")]
+    assert 1 <= len(apply) <= 2, names
+    assert all(n == ("k_rs_jitw_passes(decode)" if e > 64 else "k_rs_jit16x4(decode)") for n in apply), names

@@ -349,50 +349,76 @@ def emitw(k, e, coef):
 WIDE = {16: (6, 6848), 12: (6, 5312), 10: (5, 3776)}
 
 
+def wide_passes(e):
+    """rs_jit.h wide_passes: e > 64 rows as passes of <= 64, split evenly."""
+    return (e + 63) // 64 if e > 64 else 1
+
+
+def wide_pass_row0(e, p):
+    return p * e // wide_passes(e)
+
+
+def pass_bytes(k, rows):
+    cs, stride = WIDE[wide_rows(rows)]
+    return wide_waves(rows) * ((k + cs - 1) // cs) * stride
+
+
 @pytest.mark.parametrize("k,e", [(64, 32), (25, 25), (100, 30), (13, 27), (218, 32),
                                  (100, 20), (17, 17), (64, 19), (230, 20), (48, 24), (21, 21), (226, 24),
-                                 (100, 50), (128, 64), (186, 64), (60, 40), (70, 45), (40, 33)])
+                                 (100, 50), (128, 64), (186, 64), (60, 40), (70, 45), (40, 33),
+                                 # e > 64: passes of <= 64 rows
+                                 (150, 100), (125, 125), (185, 65), (130, 120), (160, 90)])
 def test_generated_wide_block_decodes(k, e):
     """k_rs_jitw's code (rs_jit.h Wide: 2 waves x R rows for e <= 32, 4
     waves for 32 < e <= 64, rows split evenly, chunks of CS sources, each source
-    loading its own planes, accumulators from v40): every accumulator equals
+    loading its own planes, accumulators from v40; e > 64 as passes of <= 64
+    rows, each in the layout of its own row count): every accumulator equals
     sum_q c[row][q] * src_q over GF(2^8), only the allowed instructions
     appear, every register is read after its LDS load was waited for, and
     each chunk returns right after its last source."""
-    R, nv = wide_rows(e), wide_waves(e)
-    cs, stride = WIDE[R]
     rng = random.Random(k * 7 + e)
     coef = np.array([[rng.randrange(256) for _ in range(k)] for _ in range(e)], np.uint8)
     coef[1, 2] = 0
     code = emitw(k, e, coef).tobytes()
-    nch = (k + cs - 1) // cs
-    assert len(code) == nv * nch * stride
+    passes = [(wide_pass_row0(e, p), wide_pass_row0(e, p + 1) - wide_pass_row0(e, p))
+              for p in range(wide_passes(e))]
+    assert all(0 < rows <= 64 for _, rows in passes)
+    assert len(code) == sum(pass_bytes(k, rows) for _, rows in passes)
     src = [[rng.randrange(256) for _ in range(32)] for _ in range(k)]
-    for w in range(nv):
-        nslot = wide_row0(e, w + 1) - wide_row0(e, w)
-        assert 0 < nslot <= R
-        regs = {r: 0 for r in range(256)}
-        pending = []
-        for ch in range(nch):
-            base = (w * nch + ch) * stride
-            nt = min(cs, k - cs * ch)
-            end = base + nt * (112 + 64 * nslot)
-            ins = disasm(code[base:end + 4])
-            lds = {}
-            for t in range(nt):
-                p = planes(src[cs * ch + t])
-                for a in range(8):
-                    lds[t * 2048 + (a // 4) * 1024 + 4 * (a % 4)] = p[a]
-            ret = run_chunk(ins, regs, lds, pending, addr_reg="v9")
-            assert base + ret == end, "the return sits right after the last source"
-            assert not pending, "a load left outstanding at the return"
-            used = [int(n) for _, _, ops in ins for n in re.findall(r"v\[?(\d+)", ops)]
-            used += [int(n) for _, _, ops in ins for n in re.findall(r"v\[\d+:(\d+)\]", ops)]
-            assert max(used) < 40 + 8 * R and min(used) >= 9, "register outside the kernel's v9..v(40+8R-1)"
-        for s in range(nslot):
-            row = wide_row0(e, w) + s
-            want = [0] * 32
-            for q in range(k):
-                want = [x ^ g.gf_mul(int(coef[row, q]), y) for x, y in zip(want, src[q])]
-            got = unplanes([regs[40 + 8 * s + b] for b in range(8)])
-            assert got == want, (k, e, row)
+    done = set()
+    off = 0
+    for prow0, rows in passes:
+        R, nv = wide_rows(rows), wide_waves(rows)
+        cs, stride = WIDE[R]
+        nch = (k + cs - 1) // cs
+        for w in range(nv):
+            nslot = wide_row0(rows, w + 1) - wide_row0(rows, w)
+            assert 0 < nslot <= R
+            regs = {r: 0 for r in range(256)}
+            pending = []
+            for ch in range(nch):
+                base = off + (w * nch + ch) * stride
+                nt = min(cs, k - cs * ch)
+                end = base + nt * (112 + 64 * nslot)
+                ins = disasm(code[base:end + 4])
+                lds = {}
+                for t in range(nt):
+                    p = planes(src[cs * ch + t])
+                    for a in range(8):
+                        lds[t * 2048 + (a // 4) * 1024 + 4 * (a % 4)] = p[a]
+                ret = run_chunk(ins, regs, lds, pending, addr_reg="v9")
+                assert base + ret == end, "the return sits right after the last source"
+                assert not pending, "a load left outstanding at the return"
+                used = [int(n) for _, _, ops in ins for n in re.findall(r"v\[?(\d+)", ops)]
+                used += [int(n) for _, _, ops in ins for n in re.findall(r"v\[\d+:(\d+)\]", ops)]
+                assert max(used) < 40 + 8 * R and min(used) >= 9, "register outside the kernel's v9..v(40+8R-1)"
+            for s in range(nslot):
+                row = prow0 + wide_row0(rows, w) + s
+                want = [0] * 32
+                for q in range(k):
+                    want = [x ^ g.gf_mul(int(coef[row, q]), y) for x, y in zip(want, src[q])]
+                got = unplanes([regs[40 + 8 * s + b] for b in range(8)])
+                assert got == want, (k, e, row)
+                done.add(row)
+        off += pass_bytes(k, rows)
+    assert done == set(range(e)), "every row in exactly one pass"

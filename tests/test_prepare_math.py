@@ -70,7 +70,9 @@ def orc():
     return Oracle()
 
 
-@pytest.mark.parametrize("k,e", [(64, 32), (16, 4), (100, 20), (20, 7), (5, 4), (64, 16), (9, 9), (40, 1)])
+@pytest.mark.parametrize("k,e", [(64, 32), (16, 4), (100, 20), (20, 7), (5, 4), (64, 16), (9, 9), (40, 1),
+                                 # e >= 64: Lambda's e + 1 coefficients built through LDS
+                                 (186, 64), (150, 100), (125, 125), (160, 65)])
 def test_closed_form_equals_inverse_rows(orc, k, e):
     rng = random.Random(k * 100 + e)
     for _ in range(6):
