@@ -265,11 +265,12 @@ int jit_ensure(rsgpu_ctx* ctx, size_t bytes)
 
 // The shared program of a matrix (jit_prog.h, composites by greedy cover):
 // for 16 < rows <= 64 in the two- / four-wave layout of the decode (k_rs_jitw: a
-// source's composites built twice or four times per tile), else the 8-row
-// layout (k_rs_jit).
+// source's composites built twice or four times per tile), above 64 rows in
+// passes of <= 64 in that layout (one program per pass, concatenated), else
+// the 8-row layout (k_rs_jit).
 int shared_program(rsgpu_ctx* ctx, const uint8_t* coef, int k, int rows)
 {
-    const bool wide = jitw_rows(rows) != 0;
+    const bool wide = jitw_layout(rows);
     std::vector<uint8_t> key(9 + (size_t)k * rows);
     std::memcpy(key.data(), &k, 4);
     std::memcpy(key.data() + 4, &rows, 4);
@@ -281,8 +282,17 @@ int shared_program(rsgpu_ctx* ctx, const uint8_t* coef, int k, int rows)
         return fail(ctx, RSGPU_ERR_UNSUPPORTED, "no executable device memory pool");
     int stride = 0;
     std::vector<uint8_t> code;
+    std::vector<std::pair<size_t, int>> passes;
     if (wide) {
-        code = jit::build_matrix_code_wide(coef, k, rows, jitw_rows(rows), jitw_cs(rows), &stride);
+        for (int p = 0; p < jit::wide_passes(rows); ++p) {
+            const int r0 = jit::wide_pass_row0(rows, p), pr = jit::wide_pass_rows(rows, p);
+            const std::vector<uint8_t> c =
+                jit::build_matrix_code_wide(coef + (size_t)r0 * k, k, pr, jitw_rows(pr), jitw_cs(pr), &stride);
+            if (c.empty())
+                return fail(ctx, RSGPU_ERR_UNSUPPORTED, "shared program: rows exceed the layout");
+            passes.push_back({code.size(), stride});
+            code.insert(code.end(), c.begin(), c.end());
+        }
     } else {
         code = jit::build_matrix_code(coef, k, rows, &stride);
     }
@@ -318,6 +328,7 @@ int shared_program(rsgpu_ctx* ctx, const uint8_t* coef, int k, int rows)
     RS_HIP(ctx, launch_jit_copy(ctx->d_enc_code, ctx->d_code_stage, code.size(), ctx->stream));
     ctx->enc_key = key;
     ctx->enc_chunk_stride = stride;
+    ctx->enc_passes = passes;
     return RSGPU_OK;
 }
 
@@ -330,21 +341,23 @@ int shared_program_launch(rsgpu_ctx* ctx, const uint8_t* coef, int k, int rows, 
     int rc = shared_program(ctx, coef, k, rows);
     if (rc)
         return rc;
-    if (jitw_rows(rows)) {  // one launch of the two-wave kernel, every block on the same code
-        JitArgs j{};
-        j.srcs = d_srcs;
-        j.dsts = d_dsts;
-        j.code = (const uint8_t*)ctx->d_enc_code;
-        j.chunk_stride = ctx->enc_chunk_stride;
-        j.block_stride = 0;
-        j.k = k;
-        j.rows = rows;
-        j.dst_stride = rows;
-        j.len = len;
-        j.status = nullptr;
-        j.tiles_per_wg = 2;
-        KTimer kt(ctx, name, (size_t)blocks);
-        RS_HIP(ctx, launch_rs_jitw(j, blocks, ctx->stream));
+    if (jitw_layout(rows)) {  // the two- / four-wave kernel, every block on the same code
+        for (int p = 0; p < jit::wide_passes(rows); ++p) {  // one pass up to 64 rows
+            JitArgs j{};
+            j.srcs = d_srcs;
+            j.dsts = d_dsts + jit::wide_pass_row0(rows, p);
+            j.code = (const uint8_t*)ctx->d_enc_code + ctx->enc_passes[p].first;
+            j.chunk_stride = ctx->enc_passes[p].second;
+            j.block_stride = 0;
+            j.k = k;
+            j.rows = jit::wide_pass_rows(rows, p);
+            j.dst_stride = rows;
+            j.len = len;
+            j.status = nullptr;
+            j.tiles_per_wg = 2;
+            KTimer kt(ctx, name, (size_t)blocks);
+            RS_HIP(ctx, launch_rs_jitw(j, blocks, ctx->stream));
+        }
         return RSGPU_OK;
     }
     const int nch = (k + 7) / 8;

@@ -50,6 +50,8 @@ struct rsgpu_ctx {
     size_t enc_code_bytes = 0;
     std::vector<uint8_t> enc_key;
     int enc_chunk_stride = 0;
+    // the wide layout's passes (rows > 64): (code offset, chunk stride) each
+    std::vector<std::pair<size_t, int>> enc_passes;
     void* d_code_stage = nullptr;
     size_t code_stage_bytes = 0;
     std::string err;

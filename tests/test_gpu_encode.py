@@ -58,6 +58,8 @@ def encode_and_check(ctx, orc, k, e, L, B, coef=None, seed=5, pitch=None):
 @pytest.mark.parametrize("k,e,L,B", [(64, 32, 65536, 3), (16, 4, 32000, 2), (100, 20, 8192, 2),
                                      (32, 16, 4096, 5), (128, 64, 2048, 2), (9, 40, 1024, 2),
                                      (20, 13, 96, 3), (250 - 37, 37, 64, 2),
+                                     # more than 64 rows: passes of <= 64 in the wide layout
+                                     (150, 100, 4096, 2), (125, 125, 2048, 2), (160, 65, 8192, 2),
                                      # the other compiled codes (k_rs_bs, source 0 pairing)
                                      (16, 8, 8192, 2), (64, 16, 4096, 2), (5, 4, 2048, 3), (20, 7, 4096, 2)],
                          ids=str)
