@@ -499,6 +499,7 @@ def alg_bytes(k, e, L):
     (k + e) L for an encode or a decode (read k rows, write e)."""
     blk_op = float((k + e) * L)
     return {"k_rs_bs(encode)": blk_op, "k_rs_bs_split(encode)": blk_op, "k_rs_tc_fused(decode)": blk_op,
+            "k_rs_syn_split(decode)": blk_op,
             "k_rs_encode_lh": blk_op, "k_dot_generic": blk_op,
             "k_dot_generic(decode)": blk_op,
             "k_rs_tc(encode)": blk_op, "k_rs_tc(decode)": blk_op, "k_rs_jit(decode)": blk_op,

@@ -427,6 +427,193 @@ hipError_t launch_split(const uint8_t* src, uint8_t* out, long long pitch, long 
     return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// Small decode batches of a single-chunk compiled code (C2: one block of
+// (16, 4, 1e6)): syndromes through the encode's compile-time programs, then
+// the e x e solve with runtime coefficients, in ONE launch.
+//
+// isa.cpp:169-213 applies rows of inv(b); the erased originals E also solve
+// d_E = V_E^-1 s with s = P ^ V_Ebar d_Ebar (the same unique
+// bytes).  V_Ebar holds the code's own entries 2^(p j), so each surviving
+// original goes through consume<> exactly as in the encode (a uniform branch
+// skips an erased one) and the parity rows are XORed in: no closed form and
+// no threaded code for the e x k part.  Row i of V_E^-1 is [z^p] Q_i(z) / w_i,
+// Q_i = prod_{l != i} (z + a_l), a_l = 2^(j_l), w_i = Q_i(a_i), built
+// lane-parallel while the sources fly (lane 8 i + m: [z^m] Q_i, as
+// k_rs_tc_fused builds its parity coefficients).  A runtime coefficient c
+// applies through its 8 x 8 bit matrix: plane b of c x is the XOR over a of
+// plane a of x where bit b of c 2^a is set, one v_bitop3 (out ^ (s & mask),
+// mask an SGPR of 0 or ~0) per (a, b).  Four waves per 2 KB tile split the
+// sources as k_rs_bs_split; the partial syndromes meet in LDS.
+alignas(16) __device__ const GfTables kGfBs = make_gf_tables();
+
+template <class F, int K, int E, int SPL, int G>
+__device__ __forceinline__ void syn_group(const SynArgs& a, unsigned long long emask, long long loff,
+                                          uint32_t (&acc)[E][8], F&& between)
+{
+    using P = PlanHolder<K, E, K>;
+    const int b = blockIdx.y;
+    const uint8_t* sb = a.src + (size_t)b * K * a.pitch;
+    constexpr int NT = (K - G + SPL - 1) / SPL;  // this wave's sources T = G, G + SPL, ...
+    constexpr int NP = (E - G + SPL - 1) / SPL;  // its parity rows p = G, G + SPL, ...
+    uint32_t W[NT][8];
+    uint32_t Pw[NP > 0 ? NP : 1][8];
+    // every load in flight at once; an erased original is never read
+#pragma unroll
+    for (int i = 0; i < NT; ++i)
+        load32(sb + (size_t)(G + SPL * i) * a.pitch, loff, !((emask >> (G + SPL * i)) & 1), W[i]);
+#pragma unroll
+    for (int i = 0; i < NP; ++i)
+        load32(a.par + ((size_t)b * E + G + SPL * i) * a.pitch, loff, true, Pw[i]);
+    between();  // the solve's coefficients, while the loads fly
+    const uint32_t m4 = vconst(0x0F0F0F0Fu), m2 = vconst(0x33333333u), m1 = vconst(0x55555555u);
+    const uint32_t none[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    [&]<int... Is>(std::integer_sequence<int, Is...>) {
+        (
+            [&] {
+                constexpr int T = G + SPL * Is;
+                if (!((emask >> T) & 1)) {
+                    tr8(W[Is], m4, m2, m1);
+                    consume<P, 0, E, T, false>(acc, W[Is], none);
+                }
+            }(),
+            ...);
+    }(std::make_integer_sequence<int, NT>{});
+#pragma unroll
+    for (int i = 0; i < NP; ++i) {
+        tr8(Pw[i], m4, m2, m1);
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+            acc[G + SPL * i][q] ^= Pw[i][q];
+    }
+}
+
+template <int K, int E, int SPL>
+__global__ __launch_bounds__(64 * SPL) void k_rs_syn_split(SynArgs a)
+{
+    static_assert(E <= 8 && K <= 64 && K >= SPL, "one chunk, e <= 8");
+    __shared__ uint32_t part[SPL][E * 8][64];
+    __shared__ uint32_t gtw[SPL][192];  // per wave: exp[512] | log[256]
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int b = blockIdx.y;
+    // the GF tables and the block's erasure list in one round trip
+    const uint32_t* tsrc = reinterpret_cast<const uint32_t*>(&kGfBs);
+    const uint32_t t0 = tsrc[lane], t1 = tsrc[64 + lane], t2 = tsrc[128 + lane];
+    const int j = lane < E ? a.err[(size_t)b * E + lane] : 255;  // lane i: erased original j_i
+    const int jp = __shfl_up(j, 1);
+    if (__ballot(lane < E && (j >= K || (lane > 0 && j <= jp))) != 0) {  // strictly ascending, < k
+        if (blockIdx.x == 0 && threadIdx.x == 0)
+            a.status[b] = -2;
+        return;  // uniform per workgroup
+    }
+    bool er = false;
+#pragma unroll
+    for (int i = 0; i < E; ++i)
+        er |= __builtin_amdgcn_readlane(j, i) == lane;
+    const unsigned long long emask = __ballot(lane < K && er);
+    const long long off = (long long)blockIdx.x * 2048 + lane * 32;
+    const bool inb = off + 32 <= a.len;
+    const long long loff = inb ? off : 0;  // out-of-range lanes re-read the row head
+    uint32_t* gw = gtw[wave];
+    gw[lane] = t0;
+    gw[64 + lane] = t1;
+    gw[128 + lane] = t2;
+    const uint8_t* gexp = reinterpret_cast<const uint8_t*>(gw);
+    const uint8_t* glog = gexp + 512;
+    int coef = 0;  // lane 8 i + m: (V_E^-1)[i][m]
+    auto solve_rows = [&] {
+        const int i = lane >> 3, m = lane & 7;
+        int J[8], A[8];
+#pragma unroll
+        for (int l = 0; l < 8; ++l)
+            J[l] = __builtin_amdgcn_readlane(j, l);
+        const int al = lane < E ? gexp[j] : 0;
+#pragma unroll
+        for (int l = 0; l < 8; ++l)
+            A[l] = __builtin_amdgcn_readlane(al, l);
+        int ji = 0, ai = 0;
+#pragma unroll
+        for (int l = 0; l < 8; ++l) {
+            ji = i == l ? J[l] : ji;
+            ai = i == l ? A[l] : ai;
+        }
+        const int tv = gexp[(ji + m) % 255];  // lane 8 l + c: a_l 2^c = 2^(j_l + c)
+        int qv = m == 0;                      // Q_i, one factor (z + a_l) at a time
+#pragma unroll
+        for (int l = 0; l < E; ++l) {
+            int pr = 0;  // a_l q_m from the 2^c multiples of a_l where q_m has bit c
+#pragma unroll
+            for (int c = 0; c < 8; ++c)
+                pr ^= __builtin_amdgcn_readlane(tv, l * 8 + c) & -((qv >> c) & 1);
+            int sh = __builtin_amdgcn_update_dpp(0, qv, 0x111, 0xF, 0xF, true);  // row_shr:1, q_{m-1}
+            sh = m ? sh : 0;
+            qv = l == i ? qv : (sh ^ pr);
+        }
+        int lw = 0;  // log w_i = sum_{l != i} log (a_i + a_l)
+#pragma unroll
+        for (int l = 0; l < E; ++l)
+            lw += glog[l != i ? (ai ^ A[l]) : 1];
+        coef = (i < E && m < E && qv) ? gexp[(glog[qv] + 255 * 2 - lw % 255) % 255] : 0;
+    };
+    uint32_t acc[E][8];
+#pragma unroll
+    for (int r = 0; r < E; ++r)
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+            acc[r][q] = 0;
+    [&]<int... Gs>(std::integer_sequence<int, Gs...>) {
+        ((wave == Gs ? syn_group<decltype(solve_rows)&, K, E, SPL, Gs>(a, emask, loff, acc, solve_rows) : void()),
+         ...);
+    }(std::make_integer_sequence<int, SPL>{});
+    if (blockIdx.x == 0 && threadIdx.x == 0)
+        a.status[b] = 0;
+#pragma unroll
+    for (int r = 0; r < E; ++r)
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+            part[wave][r * 8 + q][lane] = acc[r][q];
+    __syncthreads();
+    if (!inb)
+        return;
+    // wave w's output rows r = w, w + SPL, ...: out_r = sum_p c[r][p] s_p,
+    // each syndrome s_p the sum of the waves' partials
+    const uint32_t m4 = vconst(0x0F0F0F0Fu), m2 = vconst(0x33333333u), m1 = vconst(0x55555555u);
+    for (int r = wave; r < E; r += SPL) {
+        uint32_t o[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+        for (int p = 0; p < E; ++p) {
+            uint32_t sy[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                uint32_t v = 0;
+#pragma unroll
+                for (int w = 0; w < SPL; ++w)
+                    v ^= part[w][p * 8 + q][lane];
+                sy[q] = v;
+            }
+            uint32_t x = (uint32_t)__builtin_amdgcn_readlane(coef, 8 * r + p);  // c, then c 2^a
+#pragma unroll
+            for (int ab = 0; ab < 8; ++ab) {
+#pragma unroll
+                for (int bb = 0; bb < 8; ++bb)
+                    o[bb] = __builtin_amdgcn_bitop3_b32(o[bb], sy[ab], 0u - ((x >> bb) & 1u), 0x78);
+                x = ((x << 1) ^ ((x & 0x80u) ? 0x1Du : 0u)) & 0xFFu;
+            }
+        }
+        tr8(o, m4, m2, m1);
+        store32(a.out + ((size_t)b * E + r) * a.pitch, off, o);
+    }
+}
+
+template <int K, int E>
+hipError_t launch_syn(const SynArgs& a, long long blocks, hipStream_t st)
+{
+    dim3 grid((unsigned)((a.len + 2047) / 2048), (unsigned)blocks);
+    hipLaunchKernelGGL((k_rs_syn_split<K, E, 4>), grid, dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+
 template <int K, int E, int C, int NW>
 hipError_t launch(const uint8_t* src, uint8_t* out, long long pitch, long long len,
                   long long blocks, hipStream_t st)
@@ -476,6 +663,18 @@ hipError_t launch_rs_bitsliced_split(int k, int e, const uint8_t* src, uint8_t* 
     if (k == 16 && e == 8) return bs::launch_split<16, 8>(src, out, pitch, len, blocks, st);
     if (k == 5 && e == 4) return bs::launch_split<5, 4>(src, out, pitch, len, blocks, st);
     if (k == 20 && e == 7) return bs::launch_split<20, 7>(src, out, pitch, len, blocks, st);
+    return hipErrorInvalidValue;
+}
+
+hipError_t launch_rs_syn_split(int k, int e, const SynArgs& a, long long blocks, hipStream_t st)
+{
+    if (blocks <= 0 || blocks > 65535 || a.len <= 0 || a.len % 32 != 0 || !a.src || !a.par || !a.out || !a.err ||
+        !a.status)
+        return hipErrorInvalidValue;
+    if (k == 16 && e == 4) return bs::launch_syn<16, 4>(a, blocks, st);
+    if (k == 16 && e == 8) return bs::launch_syn<16, 8>(a, blocks, st);
+    if (k == 5 && e == 4) return bs::launch_syn<5, 4>(a, blocks, st);
+    if (k == 20 && e == 7) return bs::launch_syn<20, 7>(a, blocks, st);
     return hipErrorInvalidValue;
 }
 

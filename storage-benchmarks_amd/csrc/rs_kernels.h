@@ -73,6 +73,17 @@ hipError_t launch_rs_bitsliced(int k, int e, const uint8_t* src, uint8_t* out, l
 // Small batches of the single-chunk codes (16,4) (16,8) (5,4) (20,7): four
 // waves per tile split the sources (k_rs_bs_split), same bytes.
 bool rs_bitsliced_split_available(int k, int e);
+// small-batch decode of those codes in one launch: syndromes through the
+// compiled programs, the e x e solve with runtime coefficients
+struct SynArgs {
+    const uint8_t* src;  // [B][k] rows (erased ones never read)
+    const uint8_t* par;  // [B][e] rows
+    uint8_t* out;        // [B][e] rows, ascending erased order
+    const uint8_t* err;  // [B][e] erased originals, strictly ascending
+    int* status;         // [B]
+    long long pitch, len;
+};
+hipError_t launch_rs_syn_split(int k, int e, const SynArgs& a, long long blocks, hipStream_t st);
 hipError_t launch_rs_bitsliced_split(int k, int e, const uint8_t* src, uint8_t* out, long long pitch,
                                      long long len, long long blocks, hipStream_t st);
 

@@ -1409,6 +1409,22 @@ int rsgpu_decode_blocks(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch, 
     if (e > 0 && e <= 8 && k <= 64 && len > 0 && blocks > 0 &&
         decode_plan(ctx, k, e, len, pitch, blocks, d_src, d_parity, d_out) == Plan::one_matrix &&
         (long long)((len + 2047) / 2048 * blocks) < kTcSplitMaxWork) {
+        // AUTO, and a code with a compiled single-chunk program (C2's (16, 4)):
+        // syndromes through the compiled programs, the e x e solve in the same
+        // launch (k_rs_syn_split); otherwise the threaded-code one-launch decode
+        if (ctx->decode_kernel == RSGPU_DECODE_AUTO && rs_bitsliced_split_available(k, e)) {
+            SynArgs y{};
+            y.src = d_src;
+            y.par = d_parity;
+            y.out = d_out;
+            y.err = d_err;
+            y.status = d_status;
+            y.pitch = (long long)pitch;
+            y.len = (long long)len;
+            KTimer kt(ctx, "k_rs_syn_split(decode)", blocks);
+            RS_HIP(ctx, launch_rs_syn_split(k, e, y, (long long)blocks, ctx->stream));
+            return RSGPU_OK;
+        }
         TcFusedArgs f{};
         f.k = k;
         f.e = e;
