@@ -447,9 +447,21 @@ hipError_t launch_split(const uint8_t* src, uint8_t* out, long long pitch, long 
 // sources as k_rs_bs_split; the partial syndromes meet in LDS.
 alignas(16) __device__ const GfTables kGfBs = make_gf_tables();
 
+// parity rows p = G, G + SPL, ... of wave G: they survive whatever the
+// erasure list says, so their loads go out before the list arrives
+template <int E, int SPL, int G>
+__device__ __forceinline__ void syn_parity_loads(const SynArgs& a, long long loff, uint32_t (&Pw)[2][8])
+{
+    constexpr int NP = (E - G + SPL - 1) / SPL;
+    static_assert(NP <= 2, "two parity rows per wave at most");
+#pragma unroll
+    for (int i = 0; i < NP; ++i)
+        load32(a.par + ((size_t)blockIdx.y * E + G + SPL * i) * a.pitch, loff, true, Pw[i]);
+}
+
 template <class F, int K, int E, int SPL, int G>
 __device__ __forceinline__ void syn_group(const SynArgs& a, unsigned long long emask, long long loff,
-                                          uint32_t (&acc)[E][8], F&& between)
+                                          uint32_t (&acc)[E][8], uint32_t (&Pw)[2][8], F&& between)
 {
     using P = PlanHolder<K, E, K>;
     const int b = blockIdx.y;
@@ -457,14 +469,10 @@ __device__ __forceinline__ void syn_group(const SynArgs& a, unsigned long long e
     constexpr int NT = (K - G + SPL - 1) / SPL;  // this wave's sources T = G, G + SPL, ...
     constexpr int NP = (E - G + SPL - 1) / SPL;  // its parity rows p = G, G + SPL, ...
     uint32_t W[NT][8];
-    uint32_t Pw[NP > 0 ? NP : 1][8];
-    // every load in flight at once; an erased original is never read
+    // every source load in flight at once; an erased original is never read
 #pragma unroll
     for (int i = 0; i < NT; ++i)
         load32(sb + (size_t)(G + SPL * i) * a.pitch, loff, !((emask >> (G + SPL * i)) & 1), W[i]);
-#pragma unroll
-    for (int i = 0; i < NP; ++i)
-        load32(a.par + ((size_t)b * E + G + SPL * i) * a.pitch, loff, true, Pw[i]);
     between();  // the solve's coefficients, while the loads fly
     const uint32_t m4 = vconst(0x0F0F0F0Fu), m2 = vconst(0x33333333u), m1 = vconst(0x55555555u);
     const uint32_t none[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -497,6 +505,13 @@ __global__ __launch_bounds__(64 * SPL) void k_rs_syn_split(SynArgs a)
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     const int b = blockIdx.y;
+    const long long off = (long long)blockIdx.x * 2048 + lane * 32;
+    const bool inb = off + 32 <= a.len;
+    const long long loff = inb ? off : 0;  // out-of-range lanes re-read the row head
+    uint32_t Pw[2][8];
+    [&]<int... Gs>(std::integer_sequence<int, Gs...>) {
+        ((wave == Gs ? syn_parity_loads<E, SPL, Gs>(a, loff, Pw) : void()), ...);
+    }(std::make_integer_sequence<int, SPL>{});
     // the GF tables and the block's erasure list in one round trip
     const uint32_t* tsrc = reinterpret_cast<const uint32_t*>(&kGfBs);
     const uint32_t t0 = tsrc[lane], t1 = tsrc[64 + lane], t2 = tsrc[128 + lane];
@@ -512,9 +527,6 @@ __global__ __launch_bounds__(64 * SPL) void k_rs_syn_split(SynArgs a)
     for (int i = 0; i < E; ++i)
         er |= __builtin_amdgcn_readlane(j, i) == lane;
     const unsigned long long emask = __ballot(lane < K && er);
-    const long long off = (long long)blockIdx.x * 2048 + lane * 32;
-    const bool inb = off + 32 <= a.len;
-    const long long loff = inb ? off : 0;  // out-of-range lanes re-read the row head
     uint32_t* gw = gtw[wave];
     gw[lane] = t0;
     gw[64 + lane] = t1;
@@ -563,7 +575,7 @@ __global__ __launch_bounds__(64 * SPL) void k_rs_syn_split(SynArgs a)
         for (int q = 0; q < 8; ++q)
             acc[r][q] = 0;
     [&]<int... Gs>(std::integer_sequence<int, Gs...>) {
-        ((wave == Gs ? syn_group<decltype(solve_rows)&, K, E, SPL, Gs>(a, emask, loff, acc, solve_rows) : void()),
+        ((wave == Gs ? syn_group<decltype(solve_rows)&, K, E, SPL, Gs>(a, emask, loff, acc, Pw, solve_rows) : void()),
          ...);
     }(std::make_integer_sequence<int, SPL>{});
     if (blockIdx.x == 0 && threadIdx.x == 0)
