@@ -134,9 +134,9 @@ int rsgpu_encode_blocks(rsgpu_ctx *ctx, int k, int e, size_t len, size_t pitch, 
  *   GENERATED  code built on the host for the matrix, once, shared by every
  *              block: per (wave, source) only the composites its
  *              coefficients need (greedy cover); 2 waves x 16 / 12 / 10 rows
- *              for 16 < e <= 32, 4 waves for 32 < e <= 64 (k_rs_jitw, the
- *              decode's layout), else waves of 8 rows in passes of 32
- *              (k_rs_jit)
+ *              for 16 < e <= 32, 4 waves for 32 < e <= 64, passes of <= 64
+ *              rows above (k_rs_jitw, the decode's layout), else waves of 8
+ *              rows (k_rs_jit)
  *   THREADED   k_rs_tc: 256 generated handlers, one dispatch per coefficient
  * A choice that does not apply falls back in that order. */
 #define RSGPU_ENCODE_AUTO 0
@@ -159,7 +159,10 @@ size_t rsgpu_decode_workspace_bytes(int k, int e, size_t blocks);
  *               one threaded-code pass over the k - e survivors + e parity;
  *               rsgpu_decode_blocks runs a small call (< 2048 (block, 2 KB
  *               column) pairs, e <= 8, k <= 64) as ONE launch that builds the
- *               rows itself (the prepare/apply pair keeps two)
+ *               rows itself (the prepare/apply pair keeps two); under AUTO a
+ *               small call of a code with a compiled single-chunk program
+ *               ((16,4) (16,8) (5,4) (20,7)) instead runs ONE launch of
+ *               syndromes through that program plus the e x e solve
  *   GENERAL     the reference's k x k survivor-matrix inversion on the
  *               device (isa.cpp:177-204), then the decode rows; any e
  *   GENERATED   the ONE_MATRIX rows baked into per-block straight-line code
@@ -167,9 +170,10 @@ size_t rsgpu_decode_workspace_bytes(int k, int e, size_t blocks);
  *               one call per chunk of sources: 2 waves x 16 rows for
  *               24 < e <= 32 (k_rs_jit16), x 12 rows for 20 < e <= 24
  *               (k_rs_jit12), x 10 rows for 16 < e <= 20 (k_rs_jit10),
- *               4 waves of 10 / 12 / 16 rows for 32 < e <= 40 / 48 / 63
- *               (k_rs_jit{10,12,16}x4; AUTO takes it for these e too),
- *               else waves of 8 rows (k_rs_jit, e <= 16)
+ *               4 waves of 10 / 12 / 16 rows for 32 < e <= 40 / 48 / 64
+ *               (k_rs_jit{10,12,16}x4), passes of <= 64 rows for e > 64
+ *               (closed-form rows for every e; AUTO takes it for every
+ *               e > 32), else waves of 8 rows (k_rs_jit, e <= 16)
  * A choice that does not apply to a geometry falls back to GENERAL (e > 32,
  * unaligned rows) or ONE_MATRIX. */
 #define RSGPU_DECODE_AUTO 0
