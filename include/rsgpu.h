@@ -112,6 +112,23 @@ int rsgpu_ec_encode_data_update(rsgpu_ctx *ctx, int len, int k, int rows, int ve
                                 const unsigned char *gftbls, unsigned char *data,
                                 unsigned char **coding);
 
+/* The single-output / single-source members of the same ABI, as
+ * isa_arithmetic and ISA-L's own tests call them (HOST tables and pointer
+ * arrays, DEVICE rows, as rsgpu_ec_encode_data):
+ *   erasure_code.h:637 gf_vect_dot_prod (isa/ec_base.c:264-276
+ *     gf_vect_dot_prod_base): dest[i] = XOR_j c[j] * src[j][i], the 32*vlen
+ *     tables of ONE output row; any len >= 0 (ISA-L asks len >= 32).
+ *   erasure_code.h:664 gf_vect_mad (isa/ec_base.c:278-288): dest[i] ^=
+ *     c[vec_i] * src[i], tables of vec coefficients.
+ *   gf_vect_mul.h:108 gf_vect_mul (isa/ec_base.c:323-329): dest[i] =
+ *     c * src[i] with c = gftbl[1]; returns 0, or non-zero when len is not a
+ *     multiple of 32 (the dispatched ISA-L function's contract). */
+int rsgpu_gf_vect_dot_prod(rsgpu_ctx *ctx, int len, int vlen, const unsigned char *gftbls,
+                           unsigned char **src, unsigned char *dest);
+int rsgpu_gf_vect_mad(rsgpu_ctx *ctx, int len, int vec, int vec_i, const unsigned char *gftbls,
+                      unsigned char *src, unsigned char *dest);
+int rsgpu_gf_vect_mul(rsgpu_ctx *ctx, int len, const unsigned char *gftbl, void *src, void *dest);
+
 /* ---- device, batched blocks (the benchmark hot path) --------------------- */
 
 /* isa_encoder::encode_all over `blocks` independent blocks (isa.cpp:69-79):

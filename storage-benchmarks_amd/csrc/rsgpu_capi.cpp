@@ -873,6 +873,33 @@ int rsgpu_ec_encode_data_update(rsgpu_ctx* ctx, int len, int k, int rows, int ve
     return RSGPU_OK;
 }
 
+int rsgpu_gf_vect_dot_prod(rsgpu_ctx* ctx, int len, int vlen, const unsigned char* gftbls, unsigned char** src,
+                           unsigned char* dest)
+{
+    if (!ctx || len < 0 || vlen <= 0 || !gftbls || !src || !dest)
+        return fail(ctx, RSGPU_ERR_ARG, "rsgpu_gf_vect_dot_prod: bad arguments");
+    unsigned char* coding[1] = {dest};
+    return rsgpu_ec_encode_data(ctx, len, vlen, 1, gftbls, src, coding);
+}
+
+int rsgpu_gf_vect_mad(rsgpu_ctx* ctx, int len, int vec, int vec_i, const unsigned char* gftbls, unsigned char* src,
+                      unsigned char* dest)
+{
+    if (!ctx || len < 0 || vec <= 0 || vec_i < 0 || vec_i >= vec || !gftbls || !src || !dest)
+        return fail(ctx, RSGPU_ERR_ARG, "rsgpu_gf_vect_mad: bad arguments");
+    unsigned char* coding[1] = {dest};
+    return rsgpu_ec_encode_data_update(ctx, len, vec, 1, vec_i, gftbls, src, coding);
+}
+
+int rsgpu_gf_vect_mul(rsgpu_ctx* ctx, int len, const unsigned char* gftbl, void* src, void* dest)
+{
+    if (!ctx || len < 0 || len % 32 != 0 || !gftbl || !src || !dest)
+        return fail(ctx, RSGPU_ERR_ARG, "rsgpu_gf_vect_mul: len must be a multiple of 32 (gf_vect_mul.h:96-101)");
+    unsigned char* data[1] = {(unsigned char*)src};
+    unsigned char* coding[1] = {(unsigned char*)dest};
+    return rsgpu_ec_encode_data(ctx, len, 1, 1, gftbl, data, coding);
+}
+
 // ---- device, batched -----------------------------------------------------------
 
 // Most kernels put the block index in grid.y (or z), whose limit is 65535:

@@ -4,7 +4,7 @@
 // device-resident, through the ISA-L-shaped C ABI (rsgpu_ec_encode_data).
 //
 // Benchmarks (the reference's names, ISA/<name>):
-//   dot_product1        one output per call, `vectors` calls
+//   dot_product1        one output per call, `vectors` calls (rsgpu_gf_vect_dot_prod)
 //                       (gf_vect_dot_prod loop, isa_arithmetic.cpp:121-138)
 //   dot_product2        two outputs per call (gf_2vect_dot_prod_avx2 passes, :176-205)
 //   dot_product4        four outputs per call, 3/2/1 tail (gf_4vect_dot_prod_avx2, :221-257)
@@ -119,8 +119,12 @@ int main(int argc, char** argv)
                     rsgpu_ec_init_tables(v, v, &a[(size_t)v * v], g.data());
                     for (uint32_t r = 0; r < v; r += per) {
                         const int n = (int)std::min<uint32_t>(per, v - r);
-                        CHECK(rsgpu_ec_encode_data(ctx, size, v, n, &g[(size_t)r * v * 32],
-                                                   data.data(), &coding[r]));
+                        if (per == 1)  // isa_arithmetic.cpp:134 gf_vect_dot_prod
+                            CHECK(rsgpu_gf_vect_dot_prod(ctx, size, v, &g[(size_t)r * v * 32], data.data(),
+                                                         coding[r]));
+                        else
+                            CHECK(rsgpu_ec_encode_data(ctx, size, v, n, &g[(size_t)r * v * 32], data.data(),
+                                                       &coding[r]));
                     }
                     CHECK(rsgpu_synchronize(ctx));
                 };

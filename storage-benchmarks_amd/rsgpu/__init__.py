@@ -83,6 +83,9 @@ _SIGS = {
                                        C.POINTER(vp)]),
     "rsgpu_ec_encode_data_update": (C.c_int, [vp, C.c_int, C.c_int, C.c_int, C.c_int, vp, vp,
                                               C.POINTER(vp)]),
+    "rsgpu_gf_vect_dot_prod": (C.c_int, [vp, C.c_int, C.c_int, vp, C.POINTER(vp), vp]),
+    "rsgpu_gf_vect_mad": (C.c_int, [vp, C.c_int, C.c_int, C.c_int, vp, vp, vp]),
+    "rsgpu_gf_vect_mul": (C.c_int, [vp, C.c_int, vp, vp, vp]),
     "rsgpu_encode_blocks": (C.c_int, [vp, C.c_int, C.c_int, sz, sz, sz, vp, vp, vp]),
     "rsgpu_decode_workspace_bytes": (sz, [C.c_int, C.c_int, sz]),
     "rsgpu_set_decode_kernel": (C.c_int, [vp, C.c_int]),
@@ -299,6 +302,25 @@ class Context:
         self.check(lib().rsgpu_ec_encode_data_update(self._h, length, k, rows, vec_i,
                                                      g.ctypes.data, _ptr(data), cp),
                    "rsgpu_ec_encode_data_update")
+
+    def gf_vect_dot_prod(self, length: int, vlen: int, gftbls: np.ndarray, src: Sequence, dest) -> None:
+        """erasure_code.h gf_vect_dot_prod: dest = XOR_j c[j] * src[j]."""
+        sp = (vp * max(vlen, 1))(*[_ptr(x) for x in src])
+        g = np.ascontiguousarray(gftbls, np.uint8)
+        self.check(lib().rsgpu_gf_vect_dot_prod(self._h, length, vlen, g.ctypes.data, sp, _ptr(dest)),
+                   "rsgpu_gf_vect_dot_prod")
+
+    def gf_vect_mad(self, length: int, vec: int, vec_i: int, gftbls: np.ndarray, src, dest) -> None:
+        """erasure_code.h gf_vect_mad: dest ^= c[vec_i] * src."""
+        g = np.ascontiguousarray(gftbls, np.uint8)
+        self.check(lib().rsgpu_gf_vect_mad(self._h, length, vec, vec_i, g.ctypes.data, _ptr(src), _ptr(dest)),
+                   "rsgpu_gf_vect_mad")
+
+    def gf_vect_mul(self, length: int, gftbl: np.ndarray, src, dest) -> int:
+        """gf_vect_mul.h gf_vect_mul: dest = c * src; returns the status
+        (non-zero when length is not a multiple of 32, as ISA-L's)."""
+        g = np.ascontiguousarray(gftbl, np.uint8)
+        return lib().rsgpu_gf_vect_mul(self._h, length, g.ctypes.data, _ptr(src), _ptr(dest))
 
     # batched calls
     def encode_blocks(self, k, e, length, pitch, blocks, d_src, d_par, coef=None) -> None:

@@ -220,6 +220,44 @@ def test_ec_encode_data_update(ctx, orc, length):
         assert (d_out[r].cpu().numpy() == ref[r]).all()
 
 
+@pytest.mark.parametrize("length", [32, 64, 1000, 4096, 70016])
+def test_single_vector_isal_entry_points(ctx, orc, length):
+    """gf_vect_dot_prod (erasure_code.h:637, ec_base.c:264-276), gf_vect_mad
+    (:664, ec_base.c:278-288) and gf_vect_mul (gf_vect_mul.h:108,
+    ec_base.c:323-329) through the C ABI, against the oracle's base C; the
+    multiply refuses a length that is not a multiple of 32 as ISA-L's
+    dispatched function does."""
+    rng = np.random.default_rng(length + 7)
+    vlen = 9
+    coef = rng.integers(0, 256, (1, vlen), dtype=np.uint8)
+    g = orc.init_tables(vlen, 1, coef)
+    src = [rng.integers(0, 256, length, dtype=np.uint8) for _ in range(vlen)]
+    d_src = [dev(x) for x in src]
+    d_dst = torch.full((length,), 0x5A, dtype=torch.uint8, device="cuda")
+    ctx.gf_vect_dot_prod(length, vlen, g, d_src, d_dst)
+    ref = [np.zeros(length, np.uint8)]
+    orc.encode_data(length, vlen, 1, g, src, ref)
+    torch.cuda.synchronize()
+    assert (d_dst.cpu().numpy() == ref[0]).all()
+    # multiply-accumulate of source 4 into a random destination
+    start = rng.integers(0, 256, length, dtype=np.uint8)
+    d_acc = dev(start)
+    ctx.gf_vect_mad(length, vlen, 4, g, d_src[4], d_acc)
+    want = [start.copy()]
+    orc.encode_data_update(length, vlen, 1, 4, g, src[4], want)
+    torch.cuda.synchronize()
+    assert (d_acc.cpu().numpy() == want[0]).all()
+    # dest = c * src
+    tbl = orc.vect_mul_init(0x8E)
+    d_mul = torch.zeros(length, dtype=torch.uint8, device="cuda")
+    assert ctx.gf_vect_mul(length, tbl, d_src[0], d_mul) == 0
+    want = np.zeros(length, np.uint8)
+    orc.vect_mul(length, tbl, src[0], want)
+    torch.cuda.synchronize()
+    assert (d_mul.cpu().numpy() == want).all()
+    assert ctx.gf_vect_mul(length + 1, tbl, d_src[0], d_mul) != 0
+
+
 @pytest.mark.parametrize("k,e,L,B", [(16, 4, 1000000, 2), (64, 32, 1000000, 2),
                                      (100, 20, 1000000, 2), (64, 32, 32000, 64),
                                      (16, 8, 64000, 8)])
