@@ -5,6 +5,7 @@
 #   c2 c3 c4 c5   bench.py --config cN lines       line    the default bench line (+ host IO)
 #   sweep   tools/geom_sweep.sh                    bound   tools/bound_run.sh
 #   prof    tools/profile_round.sh (kernel trace, PMC traffic)   sq   tools/pmc_sq.sh
+#   arith   the isa_arithmetic peer (bin/rs_arithmetic)
 # Variants through the environment:
 #   BENCH="python3 tools/ab_lib.py --lib X.so --jitw-tiles 2"   (default: python3 bench.py)
 #   ARGS="--decode-kernel generated"   extra bench.py arguments
@@ -32,6 +33,7 @@ for step in "$@"; do
     bound) bash tools/bound_run.sh $TAG || exit 1; cat gpurun_out/bound_$TAG/summary.log ;;
     prof) bash tools/profile_round.sh $TAG || exit 1 ;;
     sq) bash tools/pmc_sq.sh $TAG || exit 1 ;;
+    arith) timeout -k 10 120 ./storage-benchmarks_amd/bin/rs_arithmetic --vectors 8 16 32 --runs 3 > $O/arithmetic.log 2>&1 || exit 1; tail -5 $O/arithmetic.log ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
