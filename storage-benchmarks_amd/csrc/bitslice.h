@@ -88,8 +88,13 @@ __device__ __forceinline__ void store32(uint8_t* row, long long off, const uint3
     v4u a, b;
     a.x = W[0]; a.y = W[1]; a.z = W[2]; a.w = W[3];
     b.x = W[4]; b.y = W[5]; b.z = W[6]; b.w = W[7];
-    *(gv4u*)(row + off) = a;
-    *(gv4u*)(row + off + 16) = b;
+    // non-temporal (`nt`): the rows are written once and not read back by
+    // this launch.  Same box, three interleaved passes (profiles/r04_nt/):
+    // C4 1262-1264 vs 1242-1246 GiB/s (generated decode 3.26 vs 3.35 ms per
+    // 4096 blocks), C5 740-741 vs 734-736, C3 1323-1326 vs 1315-1325; nt on
+    // the LDS-DMA source loads as well: C3 -1.6 % (the encode 22.7 vs 22.3 ms)
+    __builtin_nontemporal_store(a, (gv4u*)(row + off));
+    __builtin_nontemporal_store(b, (gv4u*)(row + off + 16));
 }
 
 // 16 bytes per lane global -> LDS (LDS-DMA, no VGPR destination): lane i's

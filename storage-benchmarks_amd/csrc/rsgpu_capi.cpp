@@ -122,7 +122,8 @@ struct KTimer {
     rsgpu_ctx* ctx;
     hipStream_t s;
     rsgpu_ctx::Rec rec{};
-    KTimer(rsgpu_ctx* c, const char* name, size_t blocks) : ctx(c), s(c->stream)
+    KTimer(rsgpu_ctx* c, const char* name, size_t blocks) : KTimer(c, name, blocks, c->stream) {}
+    KTimer(rsgpu_ctx* c, const char* name, size_t blocks, hipStream_t st) : ctx(c), s(st)
     {
         if (!ctx->timing)
             return;
@@ -588,7 +589,7 @@ int rsgpu_destroy(rsgpu_ctx* ctx)
         hsa_amd_memory_pool_free(ctx->d_enc_code);
     if (ctx->d_code_stage)
         (void)hipFree(ctx->d_code_stage);
-    for (hipStream_t st : {ctx->io_in, ctx->io_out})
+    for (hipStream_t st : {ctx->io_in, ctx->io_out, ctx->aux})
         if (st) {
             (void)hipStreamSynchronize(st);
             (void)hipStreamDestroy(st);
@@ -1155,6 +1156,59 @@ int emit_decode_code(rsgpu_ctx* ctx, int k, int e, size_t blocks, const uint8_t*
     return RSGPU_OK;
 }
 
+// k_rs_jitw over `blocks` blocks whose code starts at `code` (the block
+// stride jitw_code_bytes(k, e, 1)), one launch per pass of <= 64 rows (one
+// pass for e <= 64), on stream st
+int jitw_launch(rsgpu_ctx* ctx, int k, int e, size_t len, size_t blocks, const uint8_t* const* d_srcs,
+                uint8_t* const* d_dsts, const uint8_t* code, const int* d_status, hipStream_t st)
+{
+    // one launch per pass of <= 64 rows (one pass for e <= 64)
+    const size_t bs = jitw_code_bytes(k, e, 1);
+    for (int p = 0; p < jit::wide_passes(e); ++p) {
+        const int r0 = jit::wide_pass_row0(e, p), rows = jit::wide_pass_rows(e, p);
+        JitArgs j{};
+        j.srcs = d_srcs;
+        j.dsts = d_dsts + r0;
+        j.code = code + jitw_pass_offset(k, e, p);
+        j.chunk_stride = (long long)jitw_chunk_stride(rows);
+        j.block_stride = (long long)bs;
+        j.k = k;
+        j.rows = rows;
+        j.dst_stride = e;
+        j.len = (long long)len;
+        j.status = d_status;
+        // each XCD a contiguous range of (block, tile): a block's code is
+        // fetched into one L2, not eight -- 3.7 % faster at C3 for the
+        // 16-row kernel (23.3 vs 24.2 ms, profiles/r02_ab/jit_rows16/xcd_*.log),
+        // where the 8-row kernel measured 1 % slower
+        j.xcd_order = 1;
+        // two column tiles per workgroup: the waves with the same rows share
+        // their code's instruction-cache lines (C4 13.7 vs 14.2 ms per 16384
+        // blocks, C3 23.2-23.3 vs 23.4-23.5, C5 12.7-12.8 vs 12.8-12.9;
+        // three tiles: 20-30 % slower; profiles/r03_ab/tpw/)
+        j.tiles_per_wg = jit::wide_waves(rows) == 4 ? 1 : ctx->jitw_tpw ? ctx->jitw_tpw : 2;
+        // short rows: the block's few workgroups pull its code into L2 before
+        // the instruction fetch misses on it line by line (C4: 12.8 vs 13.7
+        // ms per 16384 blocks; C3, 245 workgroups per block, unchanged:
+        // profiles/r03_ab/prefetch/)
+        {
+            const long long wgs = ((long long)((len + 2047) / 2048) + j.tiles_per_wg - 1) / j.tiles_per_wg;
+            const long long lines = (long long)jitw_pass_bytes(k, rows) / 128;
+            j.code_prefetch = ctx->jitw_prefetch >= 0 ? ctx->jitw_prefetch : lines >= 32 * wgs;
+        }
+        const int r = jitw_rows(rows);
+        KTimer kt(ctx,
+                  e > 64  ? "k_rs_jitw_passes(decode)"
+                  : e > 32 ? (r == 16 ? "k_rs_jit16x4(decode)" : r == 12 ? "k_rs_jit12x4(decode)" : "k_rs_jit10x4(decode)")
+                  : r == 16 ? "k_rs_jit16(decode)"
+                  : r == 12 ? "k_rs_jit12(decode)"
+                            : "k_rs_jit10(decode)",
+                  blocks, st);
+        RS_HIP(ctx, launch_rs_jitw(j, (long long)blocks, st));
+    }
+    return RSGPU_OK;
+}
+
 // The per-block generated decode (rs_jit.hip) over rows e of every block:
 // k_rs_jitw in one launch (decode_code_bytes), or k_rs_jit in passes of
 // <= 32 rows: block b, pass p, wave w, chunk ch at d_jit + b block_stride +
@@ -1171,53 +1225,9 @@ int jit_decode_launch(rsgpu_ctx* ctx, int k, int e, size_t len, size_t blocks, c
         return fail(ctx, RSGPU_ERR_ARG,
                     "rsgpu_decode_apply: the generated code belongs to another prepare "
                     "(re-run rsgpu_decode_prepare for this workspace)");
-    if (jitw_layout(e)) {
-        // one launch per pass of <= 64 rows (one pass for e <= 64)
-        const size_t bs = jitw_code_bytes(k, e, 1);
-        for (int p = 0; p < jit::wide_passes(e); ++p) {
-            const int r0 = jit::wide_pass_row0(e, p), rows = jit::wide_pass_rows(e, p);
-            JitArgs j{};
-            j.srcs = d_srcs;
-            j.dsts = d_dsts + r0;
-            j.code = (const uint8_t*)ctx->d_jit + jitw_pass_offset(k, e, p);
-            j.chunk_stride = (long long)jitw_chunk_stride(rows);
-            j.block_stride = (long long)bs;
-            j.k = k;
-            j.rows = rows;
-            j.dst_stride = e;
-            j.len = (long long)len;
-            j.status = d_status;
-            // each XCD a contiguous range of (block, tile): a block's code is
-            // fetched into one L2, not eight -- 3.7 % faster at C3 for the
-            // 16-row kernel (23.3 vs 24.2 ms, profiles/r02_ab/jit_rows16/xcd_*.log),
-            // where the 8-row kernel measured 1 % slower
-            j.xcd_order = 1;
-            // two column tiles per workgroup: the waves with the same rows share
-            // their code's instruction-cache lines (C4 13.7 vs 14.2 ms per 16384
-            // blocks, C3 23.2-23.3 vs 23.4-23.5, C5 12.7-12.8 vs 12.8-12.9;
-            // three tiles: 20-30 % slower; profiles/r03_ab/tpw/)
-            j.tiles_per_wg = jit::wide_waves(rows) == 4 ? 1 : ctx->jitw_tpw ? ctx->jitw_tpw : 2;
-            // short rows: the block's few workgroups pull its code into L2 before
-            // the instruction fetch misses on it line by line (C4: 12.8 vs 13.7
-            // ms per 16384 blocks; C3, 245 workgroups per block, unchanged:
-            // profiles/r03_ab/prefetch/)
-            {
-                const long long wgs = ((long long)((len + 2047) / 2048) + j.tiles_per_wg - 1) / j.tiles_per_wg;
-                const long long lines = (long long)jitw_pass_bytes(k, rows) / 128;
-                j.code_prefetch = ctx->jitw_prefetch >= 0 ? ctx->jitw_prefetch : lines >= 32 * wgs;
-            }
-            const int r = jitw_rows(rows);
-            KTimer kt(ctx,
-                      e > 64  ? "k_rs_jitw_passes(decode)"
-                      : e > 32 ? (r == 16 ? "k_rs_jit16x4(decode)" : r == 12 ? "k_rs_jit12x4(decode)" : "k_rs_jit10x4(decode)")
-                      : r == 16 ? "k_rs_jit16(decode)"
-                      : r == 12 ? "k_rs_jit12(decode)"
-                                : "k_rs_jit10(decode)",
-                      blocks);
-            RS_HIP(ctx, launch_rs_jitw(j, (long long)blocks, ctx->stream));
-        }
-        return RSGPU_OK;
-    }
+    if (jitw_layout(e))
+        return jitw_launch(ctx, k, e, len, blocks, d_srcs, d_dsts, (const uint8_t*)ctx->d_jit, d_status,
+                           ctx->stream);
     const int nch = (k + 7) / 8, nwt = (e + 7) / 8;
     for (int p = 0; p * 32 < e; ++p) {
         JitArgs j{};
@@ -1319,6 +1329,85 @@ int general_apply(rsgpu_ctx* ctx, Plan plan, int k, int nerrs, size_t len, size_
     (void)pitch;
     KTimer kt(ctx, "k_dot_generic(decode)", blocks);
     RS_HIP(ctx, launch_dot_generic(a, ctx->stream));
+    return RSGPU_OK;
+}
+
+// Short-row batches of the generated decode (C4: 16 column tiles per block,
+// 16384 blocks per call): run first on the context's stream, the prepare and
+// the code emission of the whole batch (0.26 + 0.63 ms per C4 batch) hide
+// behind no kernel.  Here the batch goes in `parts` slices of whole blocks:
+// every slice's prepare and emission run on a second stream, and the context's
+// stream waits for a slice's code just before that slice's decode launch, so
+// the later slices' emission runs beside the earlier slices' decode.  Each
+// slice's code has its place in the batch's code (block b at b x the block
+// stride) and the workspace's key is the batch's: the result and the state
+// left behind are those of prepare + apply.
+constexpr size_t kPipeMinBlocks = 2048;
+constexpr size_t kPipeMaxTiles = 64;
+constexpr int kPipeParts = 4;
+
+int decode_parts(const rsgpu_ctx* ctx, int e, size_t len, size_t blocks)
+{
+    if (!jitw_layout(e) || blocks < 4)
+        return 1;
+    if (ctx->decode_pipe >= 0)
+        return std::max(1, std::min(ctx->decode_pipe, (int)(blocks / 2)));
+    return (len + 2047) / 2048 <= kPipeMaxTiles && blocks >= kPipeMinBlocks ? kPipeParts : 1;
+}
+
+int decode_pipelined(rsgpu_ctx* ctx, int parts, int k, int e, size_t len, size_t pitch, size_t blocks,
+                     const unsigned char* d_src, const unsigned char* d_parity, const unsigned char* d_err,
+                     unsigned char* d_out, void* d_workspace, int* d_status)
+{
+    int rc = jit_ensure(ctx, decode_code_bytes(k, e, blocks));
+    if (rc)
+        return rc;
+    if (!ctx->aux)
+        RS_HIP(ctx, hipStreamCreateWithFlags(&ctx->aux, hipStreamNonBlocking));
+    const WsLayout w = ws_layout(k, e, blocks);
+    char* ws = (char*)d_workspace;
+    const uint8_t** surv = (const uint8_t**)(ws + w.surv);
+    uint8_t** outp = (uint8_t**)(ws + w.outp);
+    uint8_t* coef = (uint8_t*)(ws + w.tab);
+    uint8_t* code = (uint8_t*)ctx->d_jit;
+    const size_t bs = jitw_code_bytes(k, e, 1);
+    const int r = jitw_rows(jit::wide_pass_rows(e, 0));
+    const char* emit_name = r == 16 ? "k_jit16_emit" : r == 12 ? "k_jit12_emit" : "k_jit10_emit";
+    ctx->jit_key.k = k;
+    ctx->jit_key.e = e;
+    ctx->jit_key.blocks = blocks;
+    ctx->jit_key.ws = d_workspace;
+    ctx->jit_key.gen = ++ctx->jit_gen;
+    // the second stream starts behind everything enqueued on the context's
+    // stream so far (the erasure lists, the code memory's fill, the kernels
+    // of the last call that read this workspace and code)
+    hipEvent_t start = sync_event(ctx);
+    RS_HIP(ctx, hipEventRecord(start, ctx->stream));
+    RS_HIP(ctx, hipStreamWaitEvent(ctx->aux, start, 0));
+    // slices of an even number of blocks: a slice's code starts on a 128-byte line
+    const size_t per = ((blocks + parts - 1) / parts + 1) / 2 * 2;
+    for (size_t b0 = 0; b0 < blocks; b0 += per) {
+        const size_t nb = std::min(per, blocks - b0);
+        {
+            KTimer kt(ctx, "k_decode_prepare_syn", nb, ctx->aux);
+            RS_HIP(ctx, launch_decode_prepare_syn(k, e, (long long)nb, d_err + b0 * e, d_out + b0 * e * pitch,
+                                                  (long long)pitch, surv + b0 * k, outp + b0 * e, ctx->d_tc_table,
+                                                  d_status + b0, d_src + b0 * k * pitch, d_parity + b0 * e * pitch,
+                                                  nullptr, coef + b0 * e * k, ctx->aux));
+        }
+        {
+            KTimer kt(ctx, emit_name, nb, ctx->aux);
+            RS_HIP(ctx, launch_jitw_emit(k, e, (long long)nb, coef + b0 * e * k, d_status + b0, code + b0 * bs,
+                                         ctx->aux));
+        }
+        hipEvent_t ready = sync_event(ctx);
+        RS_HIP(ctx, hipEventRecord(ready, ctx->aux));
+        RS_HIP(ctx, hipStreamWaitEvent(ctx->stream, ready, 0));
+        rc = jitw_launch(ctx, k, e, len, nb, surv + b0 * k, outp + b0 * e, code + b0 * bs, d_status + b0,
+                         ctx->stream);
+        if (rc)
+            return rc;
+    }
     return RSGPU_OK;
 }
 
@@ -1471,6 +1560,12 @@ int rsgpu_decode_blocks(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch, 
         RS_HIP(ctx, launch_rs_tc_fused(f, ctx->stream));
         return RSGPU_OK;
     }
+    // short rows, many blocks: prepare and emission beside the decode
+    if (e > 0 && len > 0 && blocks > 0 && d_workspace &&
+        decode_plan(ctx, k, e, len, pitch, blocks, d_src, d_parity, d_out) == Plan::generated)
+        if (const int parts = decode_parts(ctx, e, len, blocks); parts > 1)
+            return decode_pipelined(ctx, parts, k, e, len, pitch, blocks, d_src, d_parity, d_err, d_out,
+                                    d_workspace, d_status);
     rc = rsgpu_decode_prepare(ctx, k, e, len, pitch, blocks, d_src, d_parity, d_err, d_out,
                               d_workspace, d_status);
     if (rc)

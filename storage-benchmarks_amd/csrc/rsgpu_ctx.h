@@ -27,6 +27,10 @@ struct rsgpu_ctx {
     int decode_kernel = RSGPU_DECODE_AUTO;
     int jitw_tpw = 0;  // k_rs_jitw column tiles per workgroup (0: by geometry)
     int jitw_prefetch = -1;  // k_rs_jitw code prefetch into L2 (-1: by geometry)
+    // short-row generated decode: prepare + emission on `aux` beside the
+    // decode, in decode_pipe slices (-1: by geometry, 0 / 1: off)
+    int decode_pipe = -1;
+    hipStream_t aux = nullptr;
     // executable device memory for the generated decode code (rs_jit.h):
     // grow-only; jit_state 0 = not probed, 1 = pool found, -1 = unavailable
     void* d_jit = nullptr;

@@ -71,6 +71,17 @@ int rsgpu_internal_set_jitw_prefetch(rsgpu_ctx* ctx, int n)
     return RSGPU_OK;
 }
 
+// Test / A-B hook (not part of include/rsgpu.h): slices of the short-row
+// generated decode whose prepare and emission run beside the decode
+// (rsgpu_decode_blocks; 0 or 1 off, -1 the library's choice).
+int rsgpu_internal_set_decode_pipeline(rsgpu_ctx* ctx, int n)
+{
+    if (!ctx || n < -1 || n > 64)
+        return RSGPU_ERR_ARG;
+    ctx->decode_pipe = n;
+    return RSGPU_OK;
+}
+
 // Test hook (not in include/rsgpu.h): the host-built code of an e x k matrix
 // shared by every block (jit_prog.h, the GENERATED encode), for the CPU
 // suite to disassemble and interpret.  Returns the bytes needed, or -1;

@@ -792,6 +792,88 @@ def test_jitw_code_prefetch(ctx, k, e, L, B):
         ctx.set_decode_kernel("auto")
 
 
+def set_pipeline(ctx, n):
+    import ctypes
+    f = rsgpu.testhooks().rsgpu_internal_set_decode_pipeline
+    f.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    assert f(ctx._h, n) == 0
+
+
+@pytest.mark.parametrize("parts", [2, 3, 4])
+@pytest.mark.parametrize("k,e,L,B", [(64, 32, 32000, 9), (100, 20, 6144, 5), (48, 24, 14336, 4),
+                                     (100, 50, 32000, 6), (150, 100, 6144, 6), (64, 32, 1000000, 4)])
+def test_pipelined_decode_slices(ctx, parts, k, e, L, B):
+    """rsgpu_decode_blocks' short-row path (the A/B hook
+    rsgpu_internal_set_decode_pipeline): prepare + emission of each slice of
+    blocks on a second stream beside the decode of the slice before; the same
+    recovered bytes with the erased rows poisoned (odd block counts, slices of
+    unequal size, passes above 64 rows), one decode launch per slice and
+    pass, and a malformed list in the last slice fails that block only."""
+    ctx.set_decode_kernel("generated")
+    set_pipeline(ctx, parts)
+    try:
+        enc = rsgpu.GpuEncoder(k, L, e, blocks=B, seed=79, ctx=ctx)
+        enc.encode_all()
+        dec = rsgpu.GpuDecoder(k, L, e, blocks=B, seed=79, ctx=ctx)
+        ctx.timing_read()
+        ctx.timing_enable(True)
+        try:
+            assert decode_poisoned(ctx, enc, dec)
+            recs = ctx.timing_read()
+        finally:
+            ctx.timing_enable(False)
+        n = min(parts, B // 2)  # at most one slice per two blocks
+        per = ((B + n - 1) // n + 1) // 2 * 2
+        slices = (B + per - 1) // per
+        passes = 2 if e > 64 else 1
+        dec_recs = [r for r in recs if "(decode)" in r[0]]
+        assert len(dec_recs) == slices * passes, recs
+        assert sum(r[2] for r in dec_recs) == B * passes
+        assert sum(r[2] for r in recs if r[0] == "k_decode_prepare_syn") == B
+        bad = dec.err_host.copy()
+        bad[B - 1, :2] = bad[B - 1, 1::-1]  # not ascending
+        dec.err.copy_(torch.from_numpy(bad).view(dec.err.shape))
+        dec.decode_all(enc)
+        torch.cuda.synchronize()
+        st = dec.status.cpu().numpy()
+        assert st[B - 1] == -2 and (st[:B - 1] == 0).all(), st
+    finally:
+        set_pipeline(ctx, -1)
+        ctx.set_decode_kernel("auto")
+
+
+def test_pipelined_decode_by_default_at_c4_shape(ctx):
+    """AUTO at C4's shape (64, 32, 32000) from 2048 blocks: four slices, every
+    erased original of every block overwritten before the decode (vectorised
+    poison), all recovered; then a plain prepare + apply over the same
+    workspace agrees (the code and key left behind are the batch's)."""
+    k, e, L, B = 64, 32, 32000, 2048
+    enc = rsgpu.GpuEncoder(k, L, e, blocks=B, seed=83, ctx=ctx)
+    enc.encode_all()
+    dec = rsgpu.GpuDecoder(k, L, e, blocks=B, seed=83, ctx=ctx)
+    src = enc.src.view(B, k, enc.pitch)
+    bi = torch.arange(B, device="cuda").repeat_interleave(e)
+    ji = torch.from_numpy(dec.err_host.astype(np.int64).reshape(-1)).cuda()
+    saved = src[bi, ji, :L].clone()
+    src[bi, ji, :L] = 0xA5
+    ctx.timing_read()
+    ctx.timing_enable(True)
+    try:
+        dec.decode_all(enc)
+        torch.cuda.synchronize()
+        recs = ctx.timing_read()
+    finally:
+        ctx.timing_enable(False)
+    assert [r[2] for r in recs if r[0] == "k_rs_jit16(decode)"] == [512] * 4, recs
+    out = dec.out.view(B, e, dec.pitch)[:, :, :L].reshape(-1, L)
+    assert dec.is_complete() and torch.equal(out, saved)
+    dec.out.fill_(0)
+    ctx.decode_apply(k, e, L, dec.pitch, B, enc.src, enc.par, dec.out, dec.ws, dec.status)
+    torch.cuda.synchronize()
+    assert torch.equal(dec.out.view(B, e, dec.pitch)[:, :, :L].reshape(-1, L), saved)
+    src[bi, ji, :L] = saved
+
+
 @pytest.mark.parametrize("k,e", [(64, 32), (25, 25), (218, 32), (48, 24), (21, 21), (100, 20), (17, 17),
                                  (230, 20), (100, 50), (128, 64), (70, 45), (40, 33),
                                  (150, 100), (125, 125), (160, 65)])

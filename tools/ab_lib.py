@@ -1,11 +1,14 @@
 """Same-box A/B harness around bench.py (a tool, not the product):
 
-    python3 tools/ab_lib.py [--lib LIB.so] [--jitw-tiles N] [--jitw-prefetch N] [bench.py args...]
+    python3 tools/ab_lib.py [--lib LIB.so] [--jitw-tiles N] [--jitw-prefetch N] [--decode-pipeline N]
+                            [bench.py args...]
 
 --lib           run bench.py against another build of librsgpu.so
 --jitw-tiles    column tiles per workgroup of the two-wave generated decode
                 (1, 2, 3; 0 = the library's choice)
 --jitw-prefetch its code prefetch into L2 (0 off, 1 on, -1 the library's choice)
+--decode-pipeline  slices of the short-row generated decode with prepare and
+                emission beside the decode (0 / 1 off, -1 the library's choice)
 
 The knobs go through rsgpu_testhooks.cpp (librsgpu_testhooks.so), applied to
 every context bench.py creates; the product library exports none of them."""
@@ -24,6 +27,7 @@ def main() -> int:
     ap.add_argument("--lib", default=None)
     ap.add_argument("--jitw-tiles", type=int, default=None)
     ap.add_argument("--jitw-prefetch", type=int, default=None)
+    ap.add_argument("--decode-pipeline", type=int, default=None)
     ab, rest = ap.parse_known_args()
     if ab.lib:
         os.environ["RSGPU_LIB"] = os.path.abspath(ab.lib)
@@ -35,6 +39,8 @@ def main() -> int:
         knobs.append(("rsgpu_internal_set_jitw_tiles", ab.jitw_tiles))
     if ab.jitw_prefetch is not None:
         knobs.append(("rsgpu_internal_set_jitw_prefetch", ab.jitw_prefetch))
+    if ab.decode_pipeline is not None:
+        knobs.append(("rsgpu_internal_set_decode_pipeline", ab.decode_pipeline))
     if knobs:
         init = rsgpu.Context.__init__
 
