@@ -536,14 +536,8 @@ __global__ __launch_bounds__(256) void k_jitw_emit(int k, int e, int row_base, i
             const int acc = W::ACC + 8 * s + 2 * j;
             const uint64_t w0 = W::with_acc((uint64_t)bw[u].y << 32 | bw[u].x, acc);
             const uint64_t w1 = W::with_acc((uint64_t)bw[u].w << 32 | bw[u].z, acc + 1);
-#ifdef RSGPU_EMIT_NT
-            const bs::v4u x = {(uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1, (uint32_t)(w1 >> 32)};
-            __builtin_nontemporal_store(
-                x, &reinterpret_cast<bs::v4u*>(cbase + (size_t)ch * stride + (size_t)t * sb + W::PRE + 64 * s)[j]);
-#else
             reinterpret_cast<uint4*>(cbase + (size_t)ch * stride + (size_t)t * sb + W::PRE + 64 * s)[j] =
                 make_uint4((uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1, (uint32_t)(w1 >> 32));
-#endif
         }
     }
     // preambles: this thread's words of the table are fixed by its index mod 14
