@@ -153,7 +153,10 @@ int rsgpu_encode_blocks(rsgpu_ctx *ctx, int k, int e, size_t len, size_t pitch, 
  *              coefficients need (greedy cover); 2 waves x 16 / 12 / 10 rows
  *              for 16 < e <= 32, 4 waves for 32 < e <= 64, passes of <= 64
  *              rows above (k_rs_jitw, the decode's layout), else waves of 8
- *              rows (k_rs_jit)
+ *              rows (k_rs_jit); the context keeps the last 64 programs (at
+ *              most 256 MB of executable device memory, least recently
+ *              used out), so a caller cycling through matrices builds each
+ *              once
  *   THREADED   k_rs_tc: 256 generated handlers, one dispatch per coefficient
  * A choice that does not apply falls back in that order. */
 #define RSGPU_ENCODE_AUTO 0

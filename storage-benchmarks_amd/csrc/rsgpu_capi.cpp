@@ -259,28 +259,39 @@ int jit_ensure(rsgpu_ctx* ctx, size_t bytes)
     return RSGPU_OK;
 }
 
-// The generated code of coefficient matrix coef[rows][k] shared by every
-// block (jit_prog.h) in ctx->d_enc_code; rebuilt only when the matrix
-// changes.  Stream-ordered: the copy into the executable buffer runs after
-// every kernel enqueued before it, which may still run the old program.
-
 // The shared program of a matrix (jit_prog.h, composites by greedy cover):
 // for 16 < rows <= 64 in the two- / four-wave layout of the decode (k_rs_jitw: a
 // source's composites built twice or four times per tile), above 64 rows in
 // passes of <= 64 in that layout (one program per pass, concatenated), else
-// the 8-row layout (k_rs_jit).
-int shared_program(rsgpu_ctx* ctx, const uint8_t* coef, int k, int rows)
+// the 8-row layout (k_rs_jit).  Built on the host (~50 us for one row of 32
+// sources, ~0.3 ms for 32 x 32) and kept in a per-context LRU cache of up to
+// kProgCacheEntries programs / kProgCacheBytes, so a caller cycling through a
+// few matrices (isa_arithmetic's one-output-per-call loop: 32 rows) builds
+// each once.  Each program has its own executable buffer; an eviction waits
+// for the context's stream first (a kernel in flight may run that code).
+constexpr size_t kProgCacheEntries = 64;
+constexpr size_t kProgCacheBytes = 256u << 20;
+
+const rsgpu_ctx::SharedProg* shared_program(rsgpu_ctx* ctx, const uint8_t* coef, int k, int rows, int* rc_out)
 {
+    *rc_out = RSGPU_OK;
     const bool wide = jitw_layout(rows);
     std::vector<uint8_t> key(9 + (size_t)k * rows);
     std::memcpy(key.data(), &k, 4);
     std::memcpy(key.data() + 4, &rows, 4);
     key[8] = wide ? 1 : 0;
     std::memcpy(key.data() + 9, coef, (size_t)k * rows);
-    if (ctx->d_enc_code && key == ctx->enc_key)
-        return RSGPU_OK;
+    for (auto& pr : ctx->progs)
+        if (pr.key == key) {
+            pr.last = ++ctx->prog_tick;
+            return &pr;
+        }
+    auto err = [&](int code, const char* msg) -> const rsgpu_ctx::SharedProg* {
+        *rc_out = fail(ctx, code, msg);
+        return nullptr;
+    };
     if (jit_probe(ctx) != 1)
-        return fail(ctx, RSGPU_ERR_UNSUPPORTED, "no executable device memory pool");
+        return err(RSGPU_ERR_UNSUPPORTED, "no executable device memory pool");
     int stride = 0;
     std::vector<uint8_t> code;
     std::vector<std::pair<size_t, int>> passes;
@@ -290,47 +301,65 @@ int shared_program(rsgpu_ctx* ctx, const uint8_t* coef, int k, int rows)
             const std::vector<uint8_t> c =
                 jit::build_matrix_code_wide(coef + (size_t)r0 * k, k, pr, jitw_rows(pr), jitw_cs(pr), &stride);
             if (c.empty())
-                return fail(ctx, RSGPU_ERR_UNSUPPORTED, "shared program: rows exceed the layout");
+                return err(RSGPU_ERR_UNSUPPORTED, "shared program: rows exceed the layout");
             passes.push_back({code.size(), stride});
             code.insert(code.end(), c.begin(), c.end());
         }
     } else {
         code = jit::build_matrix_code(coef, k, rows, &stride);
     }
-    if (ctx->enc_code_bytes < code.size()) {
-        RS_HIP(ctx, hipStreamSynchronize(ctx->stream));
-        if (ctx->d_enc_code)
-            hsa_amd_memory_pool_free(ctx->d_enc_code);
-        ctx->d_enc_code = nullptr;
-        ctx->enc_code_bytes = 0;
-        void* p = nullptr;
-        if (hsa_amd_memory_pool_allocate(ctx->jit_pool, code.size(), HSA_AMD_MEMORY_POOL_EXECUTABLE_FLAG,
-                                         &p) != HSA_STATUS_SUCCESS || !p)
-            return fail(ctx, RSGPU_ERR_NOMEM, "executable device allocation failed");
-        ctx->d_enc_code = p;
-        ctx->enc_code_bytes = code.size();
+    // room: least recently used programs out, after the stream has drained
+    size_t used = 0;
+    for (const auto& pr : ctx->progs)
+        used += pr.bytes;
+    if (!ctx->progs.empty() &&
+        (ctx->progs.size() >= kProgCacheEntries || used + code.size() > kProgCacheBytes)) {
+        if (hipStreamSynchronize(ctx->stream) != hipSuccess)
+            return err(RSGPU_ERR_HIP, "shared program: draining the stream before an eviction");
+        while (!ctx->progs.empty() &&
+               (ctx->progs.size() >= kProgCacheEntries || used + code.size() > kProgCacheBytes)) {
+            auto lru = std::min_element(ctx->progs.begin(), ctx->progs.end(),
+                                        [](const auto& a, const auto& b) { return a.last < b.last; });
+            used -= lru->bytes;
+            hsa_amd_memory_pool_free(lru->code);
+            ctx->progs.erase(lru);
+        }
     }
     if (ctx->code_stage_bytes < code.size()) {
-        RS_HIP(ctx, hipStreamSynchronize(ctx->stream));
+        if (hipStreamSynchronize(ctx->stream) != hipSuccess)
+            return err(RSGPU_ERR_HIP, "shared program: draining the stream before regrowing the stage");
         if (ctx->d_code_stage)
-            RS_HIP(ctx, hipFree(ctx->d_code_stage));
+            (void)hipFree(ctx->d_code_stage);
         ctx->d_code_stage = nullptr;
-        RS_HIP(ctx, hipMalloc(&ctx->d_code_stage, code.size()));
+        ctx->code_stage_bytes = 0;
+        if (hipMalloc(&ctx->d_code_stage, code.size()) != hipSuccess)
+            return err(RSGPU_ERR_NOMEM, "shared program: code stage allocation failed");
         ctx->code_stage_bytes = code.size();
     }
+    rsgpu_ctx::SharedProg pr;
+    if (hsa_amd_memory_pool_allocate(ctx->jit_pool, code.size(), HSA_AMD_MEMORY_POOL_EXECUTABLE_FLAG,
+                                     &pr.code) != HSA_STATUS_SUCCESS || !pr.code)
+        return err(RSGPU_ERR_NOMEM, "executable device allocation failed");
+    pr.bytes = code.size();
     void* stage;
     int rc = get_stage(ctx, code.size(), &stage);
-    if (rc)
-        return rc;
-    std::memcpy(stage, code.data(), code.size());
-    rc = upload(ctx, ctx->d_code_stage, code.size());
-    if (rc)
-        return rc;
-    RS_HIP(ctx, launch_jit_copy(ctx->d_enc_code, ctx->d_code_stage, code.size(), ctx->stream));
-    ctx->enc_key = key;
-    ctx->enc_chunk_stride = stride;
-    ctx->enc_passes = passes;
-    return RSGPU_OK;
+    if (!rc) {
+        std::memcpy(stage, code.data(), code.size());
+        rc = upload(ctx, ctx->d_code_stage, code.size());
+    }
+    if (!rc && launch_jit_copy(pr.code, ctx->d_code_stage, code.size(), ctx->stream) != hipSuccess)
+        rc = fail(ctx, RSGPU_ERR_HIP, "shared program: copy into executable memory");
+    if (rc) {
+        hsa_amd_memory_pool_free(pr.code);
+        *rc_out = rc;
+        return nullptr;
+    }
+    pr.key = std::move(key);
+    pr.chunk_stride = stride;
+    pr.passes = std::move(passes);
+    pr.last = ++ctx->prog_tick;
+    ctx->progs.push_back(std::move(pr));
+    return &ctx->progs.back();
 }
 
 // dsts[b][i] = sum_j coef[i][j] srcs[b][j] through the shared generated code,
@@ -339,16 +368,17 @@ int shared_program_launch(rsgpu_ctx* ctx, const uint8_t* coef, int k, int rows, 
                           long long blocks, const uint8_t* const* d_srcs, uint8_t* const* d_dsts,
                           const char* name)
 {
-    int rc = shared_program(ctx, coef, k, rows);
-    if (rc)
+    int rc = RSGPU_OK;
+    const rsgpu_ctx::SharedProg* pg = shared_program(ctx, coef, k, rows, &rc);
+    if (!pg)
         return rc;
     if (jitw_layout(rows)) {  // the two- / four-wave kernel, every block on the same code
         for (int p = 0; p < jit::wide_passes(rows); ++p) {  // one pass up to 64 rows
             JitArgs j{};
             j.srcs = d_srcs;
             j.dsts = d_dsts + jit::wide_pass_row0(rows, p);
-            j.code = (const uint8_t*)ctx->d_enc_code + ctx->enc_passes[p].first;
-            j.chunk_stride = ctx->enc_passes[p].second;
+            j.code = (const uint8_t*)pg->code + pg->passes[p].first;
+            j.chunk_stride = pg->passes[p].second;
             j.block_stride = 0;
             j.k = k;
             j.rows = jit::wide_pass_rows(rows, p);
@@ -366,8 +396,8 @@ int shared_program_launch(rsgpu_ctx* ctx, const uint8_t* coef, int k, int rows, 
         JitArgs j{};
         j.srcs = d_srcs;
         j.dsts = d_dsts + 32 * p;
-        j.code = (const uint8_t*)ctx->d_enc_code + (size_t)p * 4 * nch * ctx->enc_chunk_stride;
-        j.chunk_stride = ctx->enc_chunk_stride;
+        j.code = (const uint8_t*)pg->code + (size_t)p * 4 * nch * pg->chunk_stride;
+        j.chunk_stride = pg->chunk_stride;
         j.block_stride = 0;
         j.k = k;
         j.rows = std::min(32, rows - 32 * p);
@@ -585,8 +615,8 @@ int rsgpu_destroy(rsgpu_ctx* ctx)
         (void)hipFree(ctx->d_tc_table);
     if (ctx->d_jit)
         hsa_amd_memory_pool_free(ctx->d_jit);
-    if (ctx->d_enc_code)
-        hsa_amd_memory_pool_free(ctx->d_enc_code);
+    for (auto& pr : ctx->progs)
+        hsa_amd_memory_pool_free(pr.code);
     if (ctx->d_code_stage)
         (void)hipFree(ctx->d_code_stage);
     for (hipStream_t st : {ctx->io_in, ctx->io_out, ctx->aux})
@@ -1355,15 +1385,37 @@ int decode_parts(const rsgpu_ctx* ctx, int e, size_t len, size_t blocks)
     return (len + 2047) / 2048 <= kPipeMaxTiles && blocks >= kPipeMinBlocks ? kPipeParts : 1;
 }
 
+int decode_slices(rsgpu_ctx* ctx, int parts, int k, int e, size_t len, size_t pitch, size_t blocks,
+                  const unsigned char* d_src, const unsigned char* d_parity, const unsigned char* d_err,
+                  unsigned char* d_out, void* d_workspace, int* d_status);
+
 int decode_pipelined(rsgpu_ctx* ctx, int parts, int k, int e, size_t len, size_t pitch, size_t blocks,
                      const unsigned char* d_src, const unsigned char* d_parity, const unsigned char* d_err,
                      unsigned char* d_out, void* d_workspace, int* d_status)
 {
-    int rc = jit_ensure(ctx, decode_code_bytes(k, e, blocks));
+    const int rc = jit_ensure(ctx, decode_code_bytes(k, e, blocks));
     if (rc)
         return rc;
     if (!ctx->aux)
         RS_HIP(ctx, hipStreamCreateWithFlags(&ctx->aux, hipStreamNonBlocking));
+    const int rs = decode_slices(ctx, parts, k, e, len, pitch, blocks, d_src, d_parity, d_err, d_out,
+                                 d_workspace, d_status);
+    // whatever the outcome, nothing enqueued on the second stream outlives
+    // the context's stream order (a failed launch leaves no emission behind
+    // that later work on the same code or workspace could race)
+    hipEvent_t done = sync_event(ctx);
+    if (hipEventRecord(done, ctx->aux) != hipSuccess || hipStreamWaitEvent(ctx->stream, done, 0) != hipSuccess) {
+        (void)hipStreamSynchronize(ctx->aux);
+        return rs ? rs : fail(ctx, RSGPU_ERR_HIP, "rsgpu_decode_blocks: joining the emission stream");
+    }
+    return rs;
+}
+
+int decode_slices(rsgpu_ctx* ctx, int parts, int k, int e, size_t len, size_t pitch, size_t blocks,
+                  const unsigned char* d_src, const unsigned char* d_parity, const unsigned char* d_err,
+                  unsigned char* d_out, void* d_workspace, int* d_status)
+{
+    int rc = RSGPU_OK;
     const WsLayout w = ws_layout(k, e, blocks);
     char* ws = (char*)d_workspace;
     const uint8_t** surv = (const uint8_t**)(ws + w.surv);

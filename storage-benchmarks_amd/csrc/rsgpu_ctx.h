@@ -46,16 +46,21 @@ struct rsgpu_ctx {
         unsigned long long gen = 0;
     } jit_key;
     hsa_amd_memory_pool_t jit_pool{};
-    // host-built code of the last shared coefficient matrix (jit_prog.h):
-    // executable copy, its key (k, rows, coefficients) and chunk stride, and
-    // the ordinary device buffer it is staged through
+    // host-built code of shared coefficient matrices (jit_prog.h), a small
+    // LRU cache: key (k, rows, layout, coefficients), executable copy, chunk
+    // stride, the wide layout's passes (rows > 64: code offset, chunk stride
+    // each); the ordinary device buffer the code is staged through
     int encode_kernel = RSGPU_ENCODE_AUTO;
-    void* d_enc_code = nullptr;
-    size_t enc_code_bytes = 0;
-    std::vector<uint8_t> enc_key;
-    int enc_chunk_stride = 0;
-    // the wide layout's passes (rows > 64): (code offset, chunk stride) each
-    std::vector<std::pair<size_t, int>> enc_passes;
+    struct SharedProg {
+        std::vector<uint8_t> key;
+        void* code = nullptr;
+        size_t bytes = 0;
+        int chunk_stride = 0;
+        std::vector<std::pair<size_t, int>> passes;
+        unsigned long long last = 0;
+    };
+    std::vector<SharedProg> progs;
+    unsigned long long prog_tick = 0;
     void* d_code_stage = nullptr;
     size_t code_stage_bytes = 0;
     std::string err;

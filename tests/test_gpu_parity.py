@@ -220,6 +220,28 @@ def test_ec_encode_data_update(ctx, orc, length):
         assert (d_out[r].cpu().numpy() == ref[r]).all()
 
 
+@pytest.mark.parametrize("k,rows", [(8, 1), (32, 1), (20, 3), (40, 24)])
+def test_shared_program_cache_cycles_matrices(ctx, orc, k, rows):
+    """rsgpu_ec_encode_data through the cached host-built programs: 70
+    different coefficient matrices (more than the 64-entry cache holds), then
+    the first ten again (rebuilt after eviction) and the last ten (cache hits),
+    each against the oracle's ec_encode_data_base on the same sources."""
+    rng = np.random.default_rng(k * 100 + rows)
+    length = 8192
+    src = [rng.integers(0, 256, length, dtype=np.uint8) for _ in range(k)]
+    d_src = [dev(x) for x in src]
+    d_out = [torch.empty(length, dtype=torch.uint8, device="cuda") for _ in range(rows)]
+    mats = [rng.integers(0, 256, (rows, k), dtype=np.uint8) for _ in range(70)]
+    for i in list(range(70)) + list(range(10)) + list(range(60, 70)):
+        g = orc.init_tables(k, rows, mats[i])
+        ctx.ec_encode_data(length, k, rows, g, d_src, d_out)
+        ref = [np.zeros(length, np.uint8) for _ in range(rows)]
+        orc.encode_data(length, k, rows, g, src, ref)
+        torch.cuda.synchronize()
+        for r in range(rows):
+            assert (d_out[r].cpu().numpy() == ref[r]).all(), (i, r)
+
+
 @pytest.mark.parametrize("length", [32, 64, 1000, 4096, 70016])
 def test_single_vector_isal_entry_points(ctx, orc, length):
     """gf_vect_dot_prod (erasure_code.h:637, ec_base.c:264-276), gf_vect_mad
