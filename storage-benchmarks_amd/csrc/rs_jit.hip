@@ -20,6 +20,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <cstring>
 #include <utility>
 
 #include "bitslice.h"
@@ -684,6 +685,27 @@ __global__ void k_jit_copy(uint64_t* dst, const uint64_t* src, long long n)
     for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
          i += (long long)gridDim.x * blockDim.x)
         dst[i] = src[i];
+}
+
+// up to PutArgs::kWords 8-byte words from the kernel arguments to device
+// memory: a small upload (a call's row pointers) without a host staging
+// buffer, its copy and the host's wait for the previous one
+__global__ void k_put_words(PutArgs a)
+{
+    if ((int)threadIdx.x < a.n)
+        a.dst[threadIdx.x] = a.w[threadIdx.x];
+}
+
+hipError_t launch_put_words(void* dst, const void* src, size_t bytes, hipStream_t st)
+{
+    if (bytes % 8 || bytes > sizeof(PutArgs::w) || !dst)
+        return hipErrorInvalidValue;
+    PutArgs a{};
+    a.dst = (uint64_t*)dst;
+    a.n = (int)(bytes / 8);
+    std::memcpy(a.w, src, bytes);
+    hipLaunchKernelGGL(k_put_words, dim3(1), dim3(PutArgs::kWords), 0, st, a);
+    return hipGetLastError();
 }
 
 hipError_t launch_jit_copy(void* dst, const void* src, size_t bytes, hipStream_t st)

@@ -143,6 +143,15 @@ size_t jitw_pass_offset(int k, int e, int p);
 hipError_t launch_jitw_emit(int k, int e, long long blocks, const uint8_t* coef, const int* status,
                             uint8_t* code, hipStream_t st);
 hipError_t launch_rs_jitw(const JitArgs& a, long long blocks, hipStream_t st);
+// small uploads through the kernel arguments (k_put_words): bytes % 8 == 0,
+// at most sizeof(PutArgs::w)
+struct PutArgs {
+    static constexpr int kWords = 128;
+    uint64_t w[kWords];
+    uint64_t* dst;
+    int n;
+};
+hipError_t launch_put_words(void* dst, const void* src, size_t bytes, hipStream_t st);
 // device-to-device copy into executable memory (host-built code staged in
 // ordinary device memory first), bytes % 8 == 0
 hipError_t launch_jit_copy(void* dst, const void* src, size_t bytes, hipStream_t st);

@@ -503,7 +503,11 @@ int dot_from_host_coef(rsgpu_ctx* ctx, const uint8_t* coef, int k, int rows, lon
 {
     const bool tcp = aligned && len % 32 == 0 && tc_ready(ctx);
     if (aligned && len % 32 == 0 && ctx->encode_kernel != RSGPU_ENCODE_THREADED && jit_probe(ctx) == 1) {
-        if (pre) {  // the row pointers the caller staged with the table upload
+        if (pre && pre_bytes <= sizeof(PutArgs::w) && pre_bytes % 8 == 0) {
+            // a few row pointers (isa_arithmetic's per-row calls): through the
+            // kernel arguments, no staging round trip
+            RS_HIP(ctx, launch_put_words(ctx->d_scratch, pre, pre_bytes, ctx->stream));
+        } else if (pre) {  // the row pointers the caller staged with the table upload
             void* stage;
             int rc = get_stage(ctx, pre_bytes, &stage);
             if (rc)
