@@ -563,6 +563,18 @@ def run_streamed(args, rsgpu, ctx, dev, rank, world, k, e, L, total_blocks):
             dec.err.view(-1)[:nb * e].copy_(h_err[i & 1][:nb].reshape(-1), non_blocking=True)
             ev_gen[i].record(s_gen)
 
+    if args.warmup > 0:
+        # one full batch untimed: the generated-code memory, the decode's
+        # second stream and the tables reach their timed size here, not in
+        # the first timed batch (a 2.46 GB executable allocation and its fill
+        # once took 2 s there, profiles/r04_lds/new_c4_2.log)
+        generate(0)
+        enc, dec = sets[0]
+        nb = min(batch, share)
+        s_cmp.wait_event(ev_gen[0])
+        ctx.encode_blocks(k, e, L, enc.pitch, nb, enc.src, enc.par)
+        ctx.decode_blocks(k, e, L, enc.pitch, nb, enc.src, enc.par, dec.err, dec.out, dec.ws, dec.status)
+        torch.cuda.synchronize()
     ctx.timing_read()
     ctx.timing_enable(True)
     torch.cuda.synchronize()
@@ -642,13 +654,6 @@ def main(argv=None):
     rank_info = None
 
     if args.config == "c4":
-        if args.warmup > 0:  # one small batch: kernels loaded, tables probed
-            w_enc = rsgpu.GpuEncoder(k, L, e, blocks=64, seed=args.seed, ctx=ctx)
-            w_dec = rsgpu.GpuDecoder(k, L, e, blocks=64, seed=args.seed, ctx=ctx)
-            w_enc.encode_all()
-            w_dec.decode_all(w_enc)
-            torch.cuda.synchronize()
-            del w_enc, w_dec
         timed, wall, bad, nbatches, batch, recs, batch_ms = run_streamed(args, rsgpu, ctx, dev, rank, world,
                                                                k, e, L, B)
         blk0, share = split(B, rank, world)
