@@ -1401,7 +1401,7 @@ int decode_pipelined(rsgpu_ctx* ctx, int parts, int k, int e, size_t len, size_t
     if (rc)
         return rc;
     if (!ctx->aux)
-        RS_HIP(ctx, hipStreamCreateWithFlags(&ctx->aux, hipStreamNonBlocking));
+        RS_HIP(ctx, rsgpu_ctx_stream_create(ctx, &ctx->aux));
     const int rs = decode_slices(ctx, parts, k, e, len, pitch, blocks, d_src, d_parity, d_err, d_out,
                                  d_workspace, d_status);
     // whatever the outcome, nothing enqueued on the second stream outlives

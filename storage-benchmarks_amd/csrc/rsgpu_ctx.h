@@ -102,6 +102,22 @@ inline int fail(rsgpu_ctx* ctx, int code, const std::string& msg)
 
 }  // namespace rsgpu
 
+// a stream of the context's device, whatever device the calling thread has
+// current (the thread's choice is restored)
+inline hipError_t rsgpu_ctx_stream_create(const rsgpu_ctx* ctx, hipStream_t* s)
+{
+    int cur = -1;
+    hipError_t e = hipGetDevice(&cur);
+    if (e != hipSuccess)
+        return e;
+    if (cur != ctx->device && (e = hipSetDevice(ctx->device)) != hipSuccess)
+        return e;
+    e = hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+    if (cur != ctx->device)
+        (void)hipSetDevice(cur);
+    return e;
+}
+
 #define RS_HIP(ctx, call)                                                                     \
     do {                                                                                      \
         hipError_t e_ = (call);                                                               \

@@ -54,9 +54,9 @@ size_t chunk_blocks(size_t bytes_per_block, size_t blocks)
 int io_setup(rsgpu_ctx* ctx, size_t bytes)
 {
     if (!ctx->io_in)
-        RS_HIP(ctx, hipStreamCreateWithFlags(&ctx->io_in, hipStreamNonBlocking));
+        RS_HIP(ctx, rsgpu_ctx_stream_create(ctx, &ctx->io_in));
     if (!ctx->io_out)
-        RS_HIP(ctx, hipStreamCreateWithFlags(&ctx->io_out, hipStreamNonBlocking));
+        RS_HIP(ctx, rsgpu_ctx_stream_create(ctx, &ctx->io_out));
     if (ctx->io_bytes < bytes) {
         if (ctx->d_io) {  // no copy or kernel of an earlier call may still use it
             RS_HIP(ctx, hipStreamSynchronize(ctx->io_in));
