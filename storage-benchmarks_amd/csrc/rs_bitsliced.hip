@@ -515,7 +515,27 @@ __global__ __launch_bounds__(64 * SPL) void k_rs_syn_split(SynArgs a)
     // the GF tables and the block's erasure list in one round trip
     const uint32_t* tsrc = reinterpret_cast<const uint32_t*>(&kGfBs);
     const uint32_t t0 = tsrc[lane], t1 = tsrc[64 + lane], t2 = tsrc[128 + lane];
-    const int j = lane < E ? a.err[(size_t)b * E + lane] : 255;  // lane i: erased original j_i
+    // lane i: erased original j_i.  The block's list through the scalar
+    // cache: the aligned words holding its E bytes (never past the word that
+    // holds the last one); C2 678-680 vs 674-676 GiB/s with a vector load,
+    // same box x4 (profiles/r04_slist/)
+    int j;
+    {
+        typedef const uint32_t __attribute__((address_space(4)))* CW;
+        const size_t base = (size_t)b * E, off = base & 3;
+        const CW wp = (CW)(a.err + (base - off));
+        constexpr int NW = (3 + E + 3) / 4;
+        uint32_t w[NW];
+#pragma unroll
+        for (int i = 0; i < NW; ++i)
+            w[i] = (off + E + 3) / 4 > (size_t)i ? wp[i] : 0u;
+        const int p = (int)off + lane;  // this lane's byte
+        uint32_t v = 0;
+#pragma unroll
+        for (int i = 0; i < NW; ++i)
+            v = (p >> 2) == i ? w[i] : v;
+        j = lane < E ? (int)((v >> (8 * (p & 3))) & 0xFFu) : 255;
+    }
     const int jp = __shfl_up(j, 1);
     if (__ballot(lane < E && (j >= K || (lane > 0 && j <= jp))) != 0) {  // strictly ascending, < k
         if (blockIdx.x == 0 && threadIdx.x == 0)
