@@ -13,9 +13,11 @@
 // per-coefficient jumps, no scalar loads of handler addresses, no GPR index
 // mode.
 //
-// The instruction cache is not invalidated between kernel launches, and the
-// code of a block is rewritten by every prepare, so wave 0 of every workgroup
-// executes s_icache_inv before the workgroup's first call.
+// The instruction cache is not invalidated between kernel launches
+// (tools/ubench_jit.hip: code rewritten between two launches runs stale
+// without it), and the code of a block is rewritten by every prepare, so
+// wave 0 of every workgroup executes s_icache_inv before the workgroup's
+// first call.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 

@@ -1159,7 +1159,7 @@ WsLayout ws_layout(int k, int e, size_t blocks)
 // Generated decode code of a call: two waves of 16 rows for 24 < e <= 32, of
 // 12 for 20 < e <= 24, of 10 for 16 < e <= 20 (rs_jit.h Wide: the composites of a source
 // built twice per tile instead of 4 or 3 times), else waves of 8 rows in
-// passes of 32.  k_rs_jit16 measured on the same boxes (tools/jit16_ab.hip,
+// passes of 32.  k_rs_jit16 measured on the same boxes (round 2's A/B build,
 // profiles/r02_ab/jit_rows16): 10 % fewer VALU instructions, 40 % fewer
 // instruction-cache misses, 3 % more cycles at 3 waves per SIMD; with the
 // XCD-contiguous order 3.7 % faster than the 8-row kernel.
