@@ -4,7 +4,9 @@
 //      (hsa_amd_memory_pool_allocate with HSA_AMD_MEMORY_POOL_EXECUTABLE_FLAG)
 //      is writable by a kernel's vector stores and callable by s_swappc;
 //   2. code rewritten at the same address between two launches is seen by
-//      the next launch (instruction cache invalidated at dispatch);
+//      the next launch when it runs s_icache_inv first (without it a run
+//      mixed old and new lines and hit an illegal instruction: the dispatch
+//      does not invalidate the instruction cache);
 //   3. the cost of STREAMING straight-line code through the instruction
 //      cache: the same number of VALU instructions run (a) from a 4 KB block
 //      called repeatedly (cache resident), (b) from one 256 KB straight-line
