@@ -522,8 +522,9 @@ __global__ __launch_bounds__(64 * SPL) void k_rs_syn_split(SynArgs a)
     int j;
     {
         typedef const uint32_t __attribute__((address_space(4)))* CW;
-        const size_t base = (size_t)b * E, off = base & 3;
-        const CW wp = (CW)(a.err + (base - off));
+        const uint8_t* lp = a.err + (size_t)b * E;  // any alignment (a slice's list)
+        const size_t off = (uintptr_t)lp & 3;
+        const CW wp = (CW)(lp - off);
         constexpr int NW = (3 + E + 3) / 4;
         uint32_t w[NW];
 #pragma unroll

@@ -746,6 +746,30 @@ def test_fused_small_decode(ctx, orc, kernel, k, e, L, B):
     ctx.set_decode_kernel("auto")
 
 
+@pytest.mark.parametrize("off", [1, 2, 3])
+@pytest.mark.parametrize("k,e", [(16, 4), (20, 7), (5, 4), (16, 8)])
+def test_small_decode_unaligned_erasure_list(ctx, off, k, e):
+    """k_rs_syn_split reads a block's list through the scalar cache by the
+    aligned words that hold it: lists at any byte offset (a slice of a larger
+    batch starts at d_err + b0 * e) decode the same, erased rows poisoned."""
+    L, B = 4096, 3
+    enc = rsgpu.GpuEncoder(k, L, e, blocks=B, seed=89, ctx=ctx)
+    enc.encode_all()
+    dec = rsgpu.GpuDecoder(k, L, e, blocks=B, seed=89, ctx=ctx)
+    buf = torch.zeros(B * e + 8, dtype=torch.uint8, device="cuda")
+    view = buf[off:off + B * e]
+    view.copy_(dec.err.view(-1))
+    dec.err = view
+    ctx.timing_read()
+    ctx.timing_enable(True)
+    try:
+        assert decode_poisoned(ctx, enc, dec)
+        names = [n for n, _, _ in ctx.timing_read()]
+    finally:
+        ctx.timing_enable(False)
+    assert names == ["k_rs_syn_split(decode)"], names
+
+
 @pytest.mark.parametrize("tpw", [2, 3])
 @pytest.mark.parametrize("k,e,L,B", [(64, 32, 1000000, 2), (64, 32, 32000, 9), (100, 20, 6144, 3),
                                      (48, 24, 14336, 2)])
