@@ -1404,6 +1404,8 @@ int decode_pipelined(rsgpu_ctx* ctx, int parts, int k, int e, size_t len, size_t
         RS_HIP(ctx, rsgpu_ctx_stream_create(ctx, &ctx->aux));
     const int rs = decode_slices(ctx, parts, k, e, len, pitch, blocks, d_src, d_parity, d_err, d_out,
                                  d_workspace, d_status);
+    if (rs)
+        ctx->jit_key.gen = 0;  // a failed call leaves no prepare behind for an apply to trust
     // whatever the outcome, nothing enqueued on the second stream outlives
     // the context's stream order (a failed launch leaves no emission behind
     // that later work on the same code or workspace could race)
