@@ -296,6 +296,85 @@ def host_io_pipelined(rsgpu, ctx, k, e, L, blocks, seed, reps=3):
             "verified": ok, "poisoned": True}
 
 
+def host_io_session(rsgpu, ctx, k, e, L, blocks, seed, chunk=4, reps=3):
+    """Goodput when the data block starts and ends in host memory and crosses
+    the link once each way: per chunk of blocks, H2D of the k source rows,
+    encode and decode on the device (the decoder reads the encoder's
+    device copy of the survivors, as isa_decoder reads the encoder's buffers,
+    isa.cpp:88, :193-197), D2H of the parity and of the recovered rows.
+    Three streams (copy-in, kernels, copy-out) over three device slots, so
+    both link directions and the kernels of consecutive chunks overlap.  Rows
+    at a pitch of exactly L.  Median of reps; bytes and verification below."""
+    import numpy as np
+    import torch
+    dev = torch.device("cuda", ctx.device)
+    pitch = L
+    h_src = torch.empty((blocks, k, L), dtype=torch.uint8, pin_memory=True)
+    h_par = torch.empty((blocks, e, L), dtype=torch.uint8, pin_memory=True)
+    h_out = torch.empty((blocks, e, L), dtype=torch.uint8, pin_memory=True)
+    probe = rsgpu.GpuEncoder(k, L, e, blocks=blocks, seed=seed, ctx=ctx)
+    h_src.copy_(probe.src.view(blocks, k, probe.pitch)[:, :, :L])
+    probe.encode_all()
+    want_par = probe.par.view(blocks, e, probe.pitch)[:, :, :L].cpu()
+    del probe
+    err_host = rsgpu.erasure_patterns(seed, 0, blocks, k, e)
+    d_err = torch.from_numpy(np.ascontiguousarray(err_host)).to(dev)
+    ws_b = rsgpu.decode_workspace_bytes(k, e, chunk)
+    slots = []
+    for _ in range(3):
+        slots.append({"src": torch.empty(chunk * k * pitch, dtype=torch.uint8, device=dev),
+                      "par": torch.empty(chunk * e * pitch, dtype=torch.uint8, device=dev),
+                      "out": torch.empty(chunk * e * pitch, dtype=torch.uint8, device=dev),
+                      "ws": torch.empty(ws_b, dtype=torch.uint8, device=dev),
+                      "st": torch.full((chunk,), -1, dtype=torch.int32, device=dev)})
+    s_in, s_cmp, s_out = torch.cuda.Stream(dev), torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    nch = (blocks + chunk - 1) // chunk
+    bad = torch.zeros(1, dtype=torch.int64, device=dev)
+    times = []
+    torch.cuda.synchronize()
+    ctx.set_stream(s_cmp.cuda_stream)
+    try:
+        for _ in range(reps):
+            ev_in = [torch.cuda.Event() for _ in range(nch)]
+            ev_cmp = [torch.cuda.Event() for _ in range(nch)]
+            ev_free = [torch.cuda.Event() for _ in range(nch)]
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for i in range(nch):
+                b0, nb = i * chunk, min(chunk, blocks - i * chunk)
+                sl = slots[i % 3]
+                with torch.cuda.stream(s_in):
+                    if i >= 3:
+                        s_in.wait_event(ev_free[i - 3])
+                    sl["src"][:nb * k * L].copy_(h_src[b0:b0 + nb].view(-1), non_blocking=True)
+                    ev_in[i].record(s_in)
+                s_cmp.wait_event(ev_in[i])
+                ctx.encode_blocks(k, e, L, pitch, nb, sl["src"], sl["par"])
+                ctx.decode_blocks(k, e, L, pitch, nb, sl["src"], sl["par"], d_err[b0:b0 + nb],
+                                  sl["out"], sl["ws"], sl["st"])
+                with torch.cuda.stream(s_cmp):
+                    bad.add_((sl["st"][:nb] != 0).sum())
+                    ev_cmp[i].record(s_cmp)
+                with torch.cuda.stream(s_out):
+                    s_out.wait_event(ev_cmp[i])
+                    h_par[b0:b0 + nb].view(-1).copy_(sl["par"][:nb * e * L], non_blocking=True)
+                    h_out[b0:b0 + nb].view(-1).copy_(sl["out"][:nb * e * L], non_blocking=True)
+                    ev_free[i].record(s_out)
+            torch.cuda.synchronize()
+            times.append(time.perf_counter() - t0)
+    finally:
+        ctx.set_torch_stream()
+    t = sorted(times)[len(times) // 2]
+    ok = int(bad.item()) == 0 and bool(torch.equal(h_par, want_par))
+    for b in range(blocks):
+        ok = ok and bool(torch.equal(h_out[b], h_src[b, torch.from_numpy(err_host[b].astype(np.int64))]))
+    out_b = e * L * blocks
+    return {"blocks": blocks, "chunk_blocks": chunk, "wall_s": t,
+            "goodput_GiBps": 2 * out_b / t / 2 ** 30,
+            "link_bytes": {"h2d": k * L * blocks, "d2h": 2 * e * L * blocks},
+            "verified": ok}
+
+
 def host_cpus():
     """CPUs this process may actually use on the box: the affinity mask,
     capped by a cgroup v2 CPU quota when one is set."""
@@ -813,6 +892,7 @@ def main(argv=None):
         line["host_io"] = host_io_rate(rsgpu, ctx, k, e, L, args.host_io, args.seed)
         line["host_io"]["pipelined"] = host_io_pipelined(rsgpu, ctx, k, e, L, args.host_io,
                                                          args.seed)
+        line["host_io"]["session"] = host_io_session(rsgpu, ctx, k, e, L, args.host_io, args.seed)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpus = host_cpus()
         threads = args.cpu_threads or cpus["usable"]

@@ -588,6 +588,18 @@ def test_host_io_ragged_chunks(ctx):
     assert s["verified"] and s["poisoned"]
 
 
+@pytest.mark.parametrize("k,e,L,B,chunk", [(64, 32, 32000, 11, 4), (16, 4, 1000000, 3, 2), (20, 7, 8192, 7, 3)])
+def test_host_io_session(ctx, k, e, L, B, chunk):
+    """bench.host_io_session (data crosses the link once each way: sources
+    in, parity and recovered rows out, three streams over three device slots):
+    ragged last chunk, slots reused; the parity equals the device path's and
+    the recovered rows the originals."""
+    sys.path.insert(0, os.path.dirname(HERE))
+    import bench
+    r = bench.host_io_session(rsgpu, ctx, k, e, L, B, seed=5, chunk=chunk, reps=1)
+    assert r["verified"] and r["blocks"] == B
+
+
 @pytest.mark.parametrize("k,e,kernel", [(64, 32, "generated"), (64, 32, "auto"), (100, 20, "generated"),
                                         (16, 4, "auto")])
 def test_full_row_every_byte_vs_oracle(ctx, orc, k, e, kernel):
