@@ -443,12 +443,15 @@ def test_bench_c2_line_prices_its_kernels():
 
 
 @pytest.mark.parametrize("kernel", ["auto", "generated", "one_matrix"])
-def test_batch_beyond_grid_limit(ctx, orc, kernel):
+@pytest.mark.parametrize("k,e", [(6, 3), (24, 20)])
+def test_batch_beyond_grid_limit(ctx, orc, kernel, k, e):
     """70000 blocks in one call (more than the 65535 a grid dimension holds):
     encode, decode (erased rows poisoned) and verify run as consecutive
-    slices; every block is verified on the device and sampled blocks on
-    either side of the slice boundary are compared with the oracle."""
-    k, e, L, B = 6, 3, 64, 70000
+    slices (for (24, 20) generated, each grid slice is decoded in the four
+    prepare + emission slices of the short-row path as well); every block is
+    verified on the device and sampled blocks on either side of the slice
+    boundary are compared with the oracle."""
+    L, B = 64, 70000
     ctx.set_decode_kernel(kernel)
     try:
         enc = rsgpu.GpuEncoder(k, L, e, blocks=B, seed=11, ctx=ctx)
