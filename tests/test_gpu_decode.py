@@ -410,6 +410,40 @@ def test_bench_under_torch_distributed_run():
     assert [(q["block0"], q["blocks"]) for q in ranks] == [(0, 4), (4, 4)]
 
 
+def test_rccl_path_single_rank():
+    """The collectives bench.py runs between ranks (barrier, all_reduce MAX of
+    the timed region, all_gather_object of the shards, all_reduce of the
+    mismatch count) on the default `nccl` backend, i.e. RCCL, in a world of
+    one rank on this GPU: the only RCCL run a one-GPU box allows (two ranks
+    cannot share a device under RCCL).  A subprocess owns the process group."""
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    code = (
+        "import os, sys, torch, torch.distributed as dist\n"
+        "sys.path.insert(0, %r)\n"
+        "import bench\n"
+        "torch.cuda.set_device(0)\n"
+        "dist.init_process_group('nccl', init_method='env://')\n"
+        "dev = torch.device('cuda', 0)\n"
+        "dist.barrier()\n"
+        "t = bench.reduce_max_time(1.25, 2, dev)\n"
+        "info = [None]\n"
+        "dist.all_gather_object(info, {'rank': 0, 'blocks': 7})\n"
+        "bad = torch.tensor([3.0], dtype=torch.float64, device=dev)\n"
+        "dist.all_reduce(bad)\n"
+        "torch.cuda.synchronize()\n"
+        "assert t == 1.25 and info[0]['blocks'] == 7 and bad.item() == 3.0, (t, info, bad)\n"
+        "print('backend', dist.get_backend())\n"
+        "dist.destroy_process_group()\n" % ROOT)
+    env = dict(os.environ, RANK="0", LOCAL_RANK="0", WORLD_SIZE="1", MASTER_ADDR="127.0.0.1",
+               MASTER_PORT=str(port))
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    assert "backend nccl" in r.stdout
+
+
 def test_bench_rejects_world_mismatch():
     env = dict(os.environ, WORLD_SIZE="1", RANK="0")
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"],
