@@ -18,7 +18,7 @@ pytestmark = pytest.mark.gpu
 
 import rsgpu  # noqa: E402
 from oracle_lib import Oracle  # noqa: E402
-from test_gpu_decode import decode_poisoned  # noqa: E402
+from test_gpu_decode import decode_poisoned, run_general  # noqa: E402
 
 ENC = ["auto", "generated", "threaded"]
 DEC = ["auto", "generated", "one_matrix", "general"]
@@ -82,3 +82,43 @@ def test_random_geometry_round_trip(ctx, orc, case):
         set_pipeline(ctx, -1)
         ctx.set_encode_kernel("auto")
         ctx.set_decode_kernel("auto")
+
+
+def draw_general(seed):
+    """A general-decode case: an RS or Cauchy m x k code, erasures among data
+    AND parity rows, rows long enough (>= 48 column tiles) for the generated
+    general decode or short for the threaded / v_perm kernels."""
+    r = np.random.default_rng(seed)
+    k = int(r.integers(2, 120))
+    p = int(r.integers(1, min(64, 250 - k) + 1))
+    n = int(r.integers(1, p + 1))
+    L = int(r.choice([131072, 98304 + 32 * int(r.integers(0, 512)), 4096, 4093]))
+    kind = "rs" if seed % 2 else "cauchy"
+    return k, p, n, L, kind
+
+
+GENERAL = [draw_general(s) for s in range(2000, 2016)]
+
+
+@pytest.mark.parametrize("case", GENERAL, ids=lambda c: "k{}p{}n{}L{}-{}".format(*c))
+def test_random_general_decode(ctx, orc, case):
+    """rsgpu_decode_general (gf_gen_decode_matrix semantics,
+    erasure_code_base_test.c:133-213) over drawn codes and erasure lists of
+    data and parity rows, erased rows poisoned, against the oracle's
+    decode_general; a singular draw must report status -1 as the reference's
+    -1 return."""
+    k, p, n, L, kind = case
+    m = k + p
+    rng = np.random.default_rng(k * 7 + p)
+    enc_m = orc.gen_rs_matrix(m, k) if kind == "rs" else orc.gen_cauchy1_matrix(m, k)
+    err = np.sort(rng.choice(m, n, replace=False)).tolist()
+    enc = rsgpu.GpuEncoder(k, L, p, blocks=1, seed=k + p, ctx=ctx)
+    ctx.encode_blocks(k, p, L, enc.pitch, 1, enc.src, enc.par, coef=enc_m[k:])
+    torch.cuda.synchronize()
+    rows = list(enc.src.view(k, enc.pitch)[:, :L].cpu().numpy()) + \
+        list(enc.par.view(p, enc.pitch)[:, :L].cpu().numpy())
+    rc, ref = orc.decode_general(enc_m, [np.ascontiguousarray(x) for x in rows], err)
+    st, rec = run_general(ctx, enc_m, enc, err, k, m, L)
+    assert st == (0 if rc == 0 else -1), (k, m, err)
+    if rc == 0:
+        assert all((rec[i] == ref[i]).all() for i in range(n)), (k, m, err)
