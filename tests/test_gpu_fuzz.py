@@ -122,3 +122,48 @@ def test_random_general_decode(ctx, orc, case):
     assert st == (0 if rc == 0 else -1), (k, m, err)
     if rc == 0:
         assert all((rec[i] == ref[i]).all() for i in range(n)), (k, m, err)
+
+
+def draw_pointer_api(seed):
+    r = np.random.default_rng(seed)
+    k = int(r.integers(1, 65))
+    rows = int(r.integers(1, 41))
+    length = int(r.choice([32 * int(r.integers(1, 2200)), int(r.integers(1, 70000))]))
+    aligned = bool(r.integers(0, 2))
+    return k, rows, length, aligned
+
+
+POINTER_API = [draw_pointer_api(s) for s in range(3000, 3016)]
+
+
+@pytest.mark.parametrize("case", POINTER_API, ids=lambda c: "k{}r{}len{}-{}".format(
+    c[0], c[1], c[2], "aligned" if c[3] else "offset"))
+def test_random_ec_encode_data(ctx, orc, case):
+    """rsgpu_ec_encode_data (erasure_code.h:98, the ISA-L argument list) over
+    drawn k, rows and lengths, with each row either 16-byte aligned or at a
+    drawn byte offset, then ec_encode_data_update of one source into the
+    same outputs: equal to the oracle's ec_encode_data_base and
+    ec_encode_data_update_base."""
+    k, rows, length, aligned = case
+    rng = np.random.default_rng(k * 100 + rows)
+    coef = rng.integers(0, 256, (rows, k), dtype=np.uint8)
+    g = orc.init_tables(k, rows, coef)
+    data = [rng.integers(0, 256, length, dtype=np.uint8) for _ in range(k)]
+    pool = torch.zeros((k + rows) * (length + 64), dtype=torch.uint8, device="cuda")
+    offs = [0 if aligned else int(rng.integers(0, 16)) for _ in range(k + rows)]
+    views = [pool[i * (length + 64) + offs[i]: i * (length + 64) + offs[i] + length] for i in range(k + rows)]
+    for i in range(k):
+        views[i].copy_(torch.from_numpy(data[i]))
+    d_data, d_out = views[:k], views[k:]
+    ctx.ec_encode_data(length, k, rows, g, d_data, d_out)
+    ref = [np.zeros(length, np.uint8) for _ in range(rows)]
+    orc.encode_data(length, k, rows, g, data, ref)
+    torch.cuda.synchronize()
+    assert all((d_out[r].cpu().numpy() == ref[r]).all() for r in range(rows))
+    vec_i = int(rng.integers(0, k))
+    upd = rng.integers(0, 256, length, dtype=np.uint8)
+    d_upd = torch.from_numpy(upd).cuda()
+    ctx.ec_encode_data_update(length, k, rows, vec_i, g, d_upd, d_out)
+    orc.encode_data_update(length, k, rows, vec_i, g, upd, ref)
+    torch.cuda.synchronize()
+    assert all((d_out[r].cpu().numpy() == ref[r]).all() for r in range(rows))
