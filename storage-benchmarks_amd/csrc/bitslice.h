@@ -141,6 +141,30 @@ __device__ __forceinline__ void glds32(const uint8_t* row, uint32_t voff, uint32
         : "memory", "scc");
 }
 
+// glds32 with the non-temporal policy: streamed sources that should not
+// displace other lines (the generated decode's code) from the XCD's L2
+__device__ __forceinline__ void glds32_nt(const uint8_t* row, uint32_t voff, uint32_t lds_lo)
+{
+    const uint64_t r = (uint64_t)row;
+    const uint64_t base = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(r >> 32)) << 32) |
+                          (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)r);
+    const uint64_t base16 = base + 16;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane(lds_lo);
+    uint32_t keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n"
+        "s_mov_b32 m0, %4\n"
+        "s_nop 0\n"
+        "global_load_lds_dwordx4 %1, %2 nt\n"
+        "s_add_u32 m0, %4, 0x400\n"
+        "s_nop 0\n"
+        "global_load_lds_dwordx4 %1, %3 nt\n"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(voff), "s"(base), "s"(base16), "s"(lo)
+        : "memory", "scc");
+}
+
 // Wave-uniform pointer from a table through the scalar cache.  (hipcc would
 // use a vector load for it -- it cannot prove the table is not written -- and
 // its vmcnt(0) would drain the LDS-DMA in flight.)

@@ -36,6 +36,7 @@ namespace jitk {
 
 using bs::barrier_lds;
 using bs::glds32;
+using bs::glds32_nt;
 using bs::sload_ptr;
 using bs::store32;
 using bs::tr8;
@@ -317,8 +318,12 @@ __global__ __launch_bounds__(64 * NV * TPW) __attribute__((amdgpu_num_vgpr(40)))
 #pragma unroll
         for (int i = 0; i < PW; ++i) {
             const int t = wave + NV * i;
-            if (t < nt)
-                glds32(p[i], loff, base + (uint32_t)(t * 2 * 64 * 16));
+            if (t < nt) {
+                if (a.code_prefetch)  // short rows: keep the block's code in L2
+                    glds32_nt(p[i], loff, base + (uint32_t)(t * 2 * 64 * 16));
+                else
+                    glds32(p[i], loff, base + (uint32_t)(t * 2 * 64 * 16));
+            }
         }
     };
     if constexpr (R == 16)
