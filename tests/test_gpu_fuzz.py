@@ -10,6 +10,8 @@ compare each recovered row with the saved original.  isa.cpp:108-229 is the
 flow; the erasure patterns are the reference's (isa.cpp:133-156, through
 rsgpu.erasure_patterns).
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -38,7 +40,8 @@ def draw(seed):
     return k, e, L, B, ENC[seed % 3], DEC[(seed // 3) % 4], int(r.choice([-1, 0, 2, 3]))
 
 
-CASES = [draw(s) for s in range(1000, 1048)]
+# RSGPU_FUZZ_N widens the draw for a one-off extended run (default 48 cases)
+CASES = [draw(s) for s in range(1000, 1000 + int(os.environ.get("RSGPU_FUZZ_N", "48")))]
 
 
 @pytest.fixture(scope="module")
