@@ -100,7 +100,7 @@ def draw_general(seed):
     return k, p, n, L, kind
 
 
-GENERAL = [draw_general(s) for s in range(2000, 2016)]
+GENERAL = [draw_general(s) for s in range(2000, 2000 + int(os.environ.get("RSGPU_FUZZ_GENERAL_N", "16")))]
 
 
 @pytest.mark.parametrize("case", GENERAL, ids=lambda c: "k{}p{}n{}L{}-{}".format(*c))
@@ -136,7 +136,7 @@ def draw_pointer_api(seed):
     return k, rows, length, aligned
 
 
-POINTER_API = [draw_pointer_api(s) for s in range(3000, 3016)]
+POINTER_API = [draw_pointer_api(s) for s in range(3000, 3000 + int(os.environ.get("RSGPU_FUZZ_API_N", "16")))]
 
 
 @pytest.mark.parametrize("case", POINTER_API, ids=lambda c: "k{}r{}len{}-{}".format(
