@@ -444,7 +444,10 @@ hipError_t launch_split(const uint8_t* src, uint8_t* out, long long pitch, long 
 // applies through its 8 x 8 bit matrix: plane b of c x is the XOR over a of
 // plane a of x where bit b of c 2^a is set, one v_bitop3 (out ^ (s & mask),
 // mask an SGPR of 0 or ~0) per (a, b).  Four waves per 2 KB tile split the
-// sources as k_rs_bs_split; the partial syndromes meet in LDS.
+// sources as k_rs_bs_split; the partial syndromes meet in LDS, each wave
+// XORing its partials into one zeroed copy (ds_xor_b32), so the output phase
+// reads every syndrome once instead of once per wave: C2 698-701 vs 687-689
+// GiB/s, same box x4 (profiles/r04_spl/ldsx_*).
 alignas(16) __device__ const GfTables kGfBs = make_gf_tables();
 
 // parity rows p = G, G + SPL, ... of wave G: they survive whatever the
@@ -500,7 +503,7 @@ template <int K, int E, int SPL>
 __global__ __launch_bounds__(64 * SPL) void k_rs_syn_split(SynArgs a)
 {
     static_assert(E <= 8 && K <= 64 && K >= SPL, "one chunk, e <= 8");
-    __shared__ uint32_t part[SPL][E * 8][64];
+    __shared__ uint32_t syn[E * 8][64];  // the syndromes: every wave's partials XORed in
     __shared__ uint32_t gtw[SPL][192];  // per wave: exp[512] | log[256]
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
@@ -512,6 +515,9 @@ __global__ __launch_bounds__(64 * SPL) void k_rs_syn_split(SynArgs a)
     [&]<int... Gs>(std::integer_sequence<int, Gs...>) {
         ((wave == Gs ? syn_parity_loads<E, SPL, Gs>(a, loff, Pw) : void()), ...);
     }(std::make_integer_sequence<int, SPL>{});
+    for (int i = threadIdx.x; i < E * 8 * 64; i += 64 * SPL)
+        (&syn[0][0])[i] = 0;
+    __syncthreads();
     // the GF tables and the block's erasure list in one round trip
     const uint32_t* tsrc = reinterpret_cast<const uint32_t*>(&kGfBs);
     const uint32_t t0 = tsrc[lane], t1 = tsrc[64 + lane], t2 = tsrc[128 + lane];
@@ -605,12 +611,12 @@ __global__ __launch_bounds__(64 * SPL) void k_rs_syn_split(SynArgs a)
     for (int r = 0; r < E; ++r)
 #pragma unroll
         for (int q = 0; q < 8; ++q)
-            part[wave][r * 8 + q][lane] = acc[r][q];
+            atomicXor(&syn[r * 8 + q][lane], acc[r][q]);  // ds_xor_b32, no return
     __syncthreads();
     if (!inb)
         return;
     // wave w's output rows r = w, w + SPL, ...: out_r = sum_p c[r][p] s_p,
-    // each syndrome s_p the sum of the waves' partials
+    // each syndrome s_p already the sum of the waves' partials
     const uint32_t m4 = vconst(0x0F0F0F0Fu), m2 = vconst(0x33333333u), m1 = vconst(0x55555555u);
     for (int r = wave; r < E; r += SPL) {
         uint32_t o[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -618,13 +624,8 @@ __global__ __launch_bounds__(64 * SPL) void k_rs_syn_split(SynArgs a)
         for (int p = 0; p < E; ++p) {
             uint32_t sy[8];
 #pragma unroll
-            for (int q = 0; q < 8; ++q) {
-                uint32_t v = 0;
-#pragma unroll
-                for (int w = 0; w < SPL; ++w)
-                    v ^= part[w][p * 8 + q][lane];
-                sy[q] = v;
-            }
+            for (int q = 0; q < 8; ++q)
+                sy[q] = syn[p * 8 + q][lane];
             uint32_t x = (uint32_t)__builtin_amdgcn_readlane(coef, 8 * r + p);  // c, then c 2^a
 #pragma unroll
             for (int ab = 0; ab < 8; ++ab) {
