@@ -46,6 +46,7 @@ sys.path.insert(0, os.path.join(ROOT, "storage-benchmarks_amd"))
 
 CONFIGS = {
     # name: (symbols, symbol_size, loss_rate, blocks per GPU)
+    "c1": (16, 64000, 0.5, 1),          # the reference's CPU plumbing case: host only, no GPU
     "c2": (16, 1000000, 0.25, 1),
     "c3": (64, 1000000, 0.5, 1024),
     "c4": (64, 32000, 0.5, 1 << 20),    # 2^20 blocks in total, streamed, split over the GPUs
@@ -73,6 +74,8 @@ def parse(argv=None):
     p.add_argument("--encode-kernel", default="auto",
                    choices=["auto", "compiled", "generated", "threaded"])
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--c1-seconds", type=float, default=4.0,
+                   help="c1: timed CPU seconds per leg (the sample size is calibrated to it)")
     p.add_argument("--cpu-threads", type=int, default=None)
     p.add_argument("--no-ref-base", action="store_true",
                    help="skip the (slow, ~10 s) reference scalar-C CPU sample")
@@ -304,7 +307,10 @@ def host_io_session(rsgpu, ctx, k, e, L, blocks, seed, chunk=4, reps=3):
     isa.cpp:88, :193-197), D2H of the parity and of the recovered rows.
     Three streams (copy-in, kernels, copy-out) over three device slots, so
     both link directions and the kernels of consecutive chunks overlap.  Rows
-    at a pitch of exactly L.  Median of reps; bytes and verification below."""
+    at a pitch of exactly L.  The erased originals of each chunk are
+    overwritten with 0xA5 on the device between its encode and its decode
+    (timed; ~0.5 % of a chunk's time), so a decode that read them would fail
+    the verification.  Median of reps; bytes and verification below."""
     import numpy as np
     import torch
     dev = torch.device("cuda", ctx.device)
@@ -319,6 +325,13 @@ def host_io_session(rsgpu, ctx, k, e, L, blocks, seed, chunk=4, reps=3):
     del probe
     err_host = rsgpu.erasure_patterns(seed, 0, blocks, k, e)
     d_err = torch.from_numpy(np.ascontiguousarray(err_host)).to(dev)
+    # per chunk, the slot rows of its erased originals (poisoned between the
+    # encode and the decode, as host_io_rate / host_io_pipelined do)
+    erased_rows = []
+    for i in range((blocks + chunk - 1) // chunk):
+        b0, nb = i * chunk, min(chunk, blocks - i * chunk)
+        rows = np.arange(nb)[:, None] * k + err_host[b0:b0 + nb].astype(np.int64)
+        erased_rows.append(torch.from_numpy(rows.reshape(-1)).to(dev))
     ws_b = rsgpu.decode_workspace_bytes(k, e, chunk)
     slots = []
     for _ in range(3):
@@ -350,6 +363,8 @@ def host_io_session(rsgpu, ctx, k, e, L, blocks, seed, chunk=4, reps=3):
                     ev_in[i].record(s_in)
                 s_cmp.wait_event(ev_in[i])
                 ctx.encode_blocks(k, e, L, pitch, nb, sl["src"], sl["par"])
+                with torch.cuda.stream(s_cmp):  # what the decoder may not read
+                    sl["src"][:nb * k * pitch].view(nb * k, pitch).index_fill_(0, erased_rows[i], 0xA5)
                 ctx.decode_blocks(k, e, L, pitch, nb, sl["src"], sl["par"], d_err[b0:b0 + nb],
                                   sl["out"], sl["ws"], sl["st"])
                 with torch.cuda.stream(s_cmp):
@@ -372,7 +387,7 @@ def host_io_session(rsgpu, ctx, k, e, L, blocks, seed, chunk=4, reps=3):
     return {"blocks": blocks, "chunk_blocks": chunk, "wall_s": t,
             "goodput_GiBps": 2 * out_b / t / 2 ** 30,
             "link_bytes": {"h2d": k * L * blocks, "d2h": 2 * e * L * blocks},
-            "verified": ok}
+            "verified": ok, "poisoned": True}
 
 
 def host_cpus():
@@ -445,6 +460,72 @@ def cpu_baseline(k, e, L, threads, kernel=1, blocks_per_thread=None, one_thread_
             "encode_s_per_block": many["encode_s_per_block"],
             "decode_s_per_block": many["decode_s_per_block"],
             "threads_1": one, "threads_nproc": many}
+
+
+def c1_line(args) -> dict:
+    """BASELINE.json configs[0]: benchmark/isa_throughput on the CPU at
+    --symbols=16 --symbol_size=64000 --loss_rate=0.5, plumbing only: the
+    engine and the GPU are never touched.  The reference's path as compiled
+    from /root/reference (oracle/_ref: gf_gen_rs_matrix, ec_init_tables,
+    gf_invert_matrix, ec_encode_data_base) and our AVX2 restatement of its
+    asm kernel, each on 1 thread (isa.cpp's single-threaded semantics) and on
+    every usable host thread (independent blocks).  Accounting as the
+    reference harness (throughput_benchmark.hpp:37-67, 179-196): encoder
+    goodput = payload_count x symbol_size / encode time (isa.cpp:38, the e
+    parity symbols), decoder goodput = erased x symbol_size / decode time;
+    `value` = both outputs over both times, as bench.py's other configs."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_lib
+    k, L, loss, _ = CONFIGS["c1"]
+    e = int(math.ceil(k * loss))
+    if not oracle_lib.have_reference():
+        raise SystemExit("bench.py --config c1 needs oracle/_ref (python __graft_entry__.py build)")
+    ref = oracle_lib.Reference()
+    cpus = host_cpus()
+    nthreads = args.cpu_threads or cpus["usable"]
+
+    def leg(kernel, threads):
+        # calibrate on a few blocks, then size the sample to --c1-seconds
+        r = ref.cpu_bench(k, e, L, threads, 4, args.seed, kernel)
+        per_block = max(r["max_thread_s"] / 4, 1e-6)
+        nb = int(min(200000, max(4, args.c1_seconds / per_block)))
+        r = ref.cpu_bench(k, e, L, threads, nb, args.seed, kernel)
+        blocks = threads * nb
+        enc, dec = r["enc_s"] / blocks, r["dec_s"] / blocks  # per block, summed over threads
+        out = e * L
+        return {"kernel": "ISA-L 2.13 ec_encode_data_base, compiled from the reference (oracle/_ref)"
+                          if kernel == 0 else "AVX2 restatement of gf_vect_dot_prod_avx2 (oracle/isal_avx2_port.c)",
+                "kind": "reference" if kernel == 0 else "port", "threads": threads,
+                "blocks_per_thread": nb, "max_thread_s": round(r["max_thread_s"], 3),
+                "failures": r["failures"],
+                "encoder_goodput_MBps": round(out / enc / 1e6, 1),
+                "decoder_goodput_MBps": round(out / dec / 1e6, 1),
+                "encode_us_per_block": round(enc * 1e6, 2), "decode_us_per_block": round(dec * 1e6, 2),
+                "goodput_GiBps": 2.0 * out * threads * nb / r["max_thread_s"] / 2 ** 30}
+
+    legs = [leg(0, 1), leg(1, 1), leg(0, nthreads), leg(1, nthreads)]
+    head = legs[0]
+    ok = all(lg["failures"] == 0 for lg in legs)
+    return {
+        "metric": "encode+decode goodput GiB/s (device-resident) at symbols x symbol_size; "
+                  "%HBM roofline",
+        "value": round(head["goodput_GiBps"], 4), "unit": "GiB/s", "n_gpus": 0,
+        "steps": head["blocks_per_thread"], "warmup": 0,
+        "ms_per_step": round((head["encode_us_per_block"] + head["decode_us_per_block"]) / 1e3, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic",
+        "config": {"workload": f"isa_throughput c1 on the host CPU (plumbing, no GPU): symbols={k} "
+                               f"symbol_size={L} loss_rate={loss} erased={e}; value = the reference's "
+                               f"compiled C on 1 thread",
+                   "symbols": k, "symbol_size": L, "loss_rate": loss, "erased": e,
+                   "parallelism": "1 thread (value); all usable threads in legs"},
+        "device": "cpu", "verified": ok, "roofline": None,
+        "cpu_baseline": {"value": round(head["goodput_GiBps"], 4), "unit": "GiB/s", "cores": 1,
+                         "kind": "reference",
+                         "sample": f"{head['blocks_per_thread']} blocks (k={k}, e={e}, L={L}) encode+decode "
+                                   f"on 1 thread, {head['max_thread_s']} s"},
+        "legs": legs, "cpu_model": cpu_model(), **cpus,
+    }
 
 
 def launch_cost(torch, n=400):
@@ -700,6 +781,9 @@ def main(argv=None):
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         # no launcher: this process only spawns the ranks (never touches the GPU)
         return spawn_ranks(args.gpus, argv)
+    if args.config == "c1":  # host only: neither torch's GPU side nor the engine
+        print(json.dumps(c1_line(args)), flush=True)
+        return 0
     rank, world, local = dist_env()
     if world != args.gpus:
         print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)

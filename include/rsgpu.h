@@ -192,8 +192,10 @@ size_t rsgpu_decode_workspace_bytes(int k, int e, size_t blocks);
  *               (k_rs_jit12), x 10 rows for 16 < e <= 20 (k_rs_jit10),
  *               4 waves of 10 / 12 / 16 rows for 32 < e <= 40 / 48 / 64
  *               (k_rs_jit{10,12,16}x4), passes of <= 64 rows for e > 64
- *               (closed-form rows for every e; AUTO takes it for every
- *               e > 32), else waves of 8 rows (k_rs_jit, e <= 16)
+ *               (closed-form rows for every e; AUTO takes it for e > 32
+ *               when the code pays for itself -- enough column tiles per
+ *               block, jit_pays -- and otherwise runs GENERAL), else waves
+ *               of 8 rows (k_rs_jit, e <= 16)
  * A choice that does not apply to a geometry falls back to GENERAL (e > 32,
  * unaligned rows) or ONE_MATRIX. */
 #define RSGPU_DECODE_AUTO 0

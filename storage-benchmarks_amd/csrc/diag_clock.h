@@ -13,6 +13,24 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+// Timing-only energy variants of the diagnostic build (round 5,
+// tools/energy_run.sh; make diag DIAG_VARIANT=n): the same instruction
+// stream with one component's data made quiet, or one phase removed.  Their
+// outputs are WRONG by construction; the product build always has 0.
+//   1 hbmq    sources read from, rows written to, a window of two blocks x
+//             16 KB per row that stays in the XCD's L2 (HBM I/O quiet)
+//   2 zplane  the transposes write zero planes (LDS plane writes and reads,
+//             the VALU of the multiply-accumulates and the row stores quiet)
+//   3 valuq   the planes are read from LDS as usual but land in dead
+//             registers, the VALU works on zero planes (VALU quiet)
+//   4 nowait  the generated decode's per-source LDS wait removed
+//   5 notr    the source transposes skipped (raw bytes used as planes)
+#if defined(RSGPU_DIAG_CLOCK) && defined(RSGPU_DIAG_VARIANT)
+#define RSGPU_DIAG_VAR RSGPU_DIAG_VARIANT
+#else
+#define RSGPU_DIAG_VAR 0
+#endif
+
 #ifdef RSGPU_DIAG_CLOCK
 namespace rsgpu {
 namespace diag {

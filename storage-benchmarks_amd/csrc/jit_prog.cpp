@@ -7,6 +7,7 @@
 #include <algorithm>
 
 #include "rs_jit.h"
+#include "rs_kernels.h"
 
 namespace rsgpu {
 namespace jit {
@@ -335,6 +336,24 @@ std::vector<uint8_t> build_matrix_code_wide(const uint8_t* c, int k, int e, int 
         for (int ch = 0; ch < nch && nslot > 0; ++ch)
             emit_chunk_wide(&code[((size_t)w * nch + ch) * stride], std::min(CS, k - CS * ch), nslot,
                             &progs[(size_t)w * k + CS * ch]);
+    }
+    return code;
+}
+
+std::vector<uint8_t> build_matrix_code_wide_passes(const uint8_t* c, int k, int e,
+                                                   std::vector<std::pair<size_t, int>>* passes, int max_ops)
+{
+    std::vector<uint8_t> code;
+    passes->clear();
+    for (int p = 0; p < wide_passes(e); ++p) {
+        const int r0 = wide_pass_row0(e, p), pr = wide_pass_rows(e, p);
+        int stride = 0;
+        const std::vector<uint8_t> cp =
+            build_matrix_code_wide(c + (size_t)r0 * k, k, pr, jitw_rows(pr), jitw_cs(pr), &stride, max_ops);
+        if (cp.empty())
+            return {};
+        passes->push_back({code.size(), stride});
+        code.insert(code.end(), cp.begin(), cp.end());
     }
     return code;
 }

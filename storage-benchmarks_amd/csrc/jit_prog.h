@@ -16,6 +16,7 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include <utility>
 #include <vector>
 
 namespace rsgpu {
@@ -65,6 +66,16 @@ std::vector<uint8_t> build_matrix_code(const uint8_t* c, int k, int e, int* chun
 // rounded to 64 bytes.
 std::vector<uint8_t> build_matrix_code_wide(const uint8_t* c, int k, int e, int R, int CS, int* chunk_stride,
                                             int max_ops = kMaxComposites);
+
+// Rows of any count the wide layout takes (16 < e <= 125): passes of <= 64
+// rows (rs_jit.h wide_passes), each built as above in the layout of its own
+// row count (jitw_rows / jitw_cs) and appended; passes[p] = (byte offset of
+// pass p, its chunk stride).  Empty when a pass fits no layout.  The
+// GENERATED encode's shared programs (rsgpu_capi.cpp shared_program) are
+// exactly this.
+std::vector<uint8_t> build_matrix_code_wide_passes(const uint8_t* c, int k, int e,
+                                                   std::vector<std::pair<size_t, int>>* passes,
+                                                   int max_ops = kMaxComposites);
 
 }  // namespace jit
 }  // namespace rsgpu

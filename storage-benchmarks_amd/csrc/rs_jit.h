@@ -41,6 +41,14 @@
 #define RJ_HD
 #endif
 
+// diagnostic energy variants (diag_clock.h): 3 lands the planes in dead
+// registers, 4 drops the per-source LDS wait; 0 in the product build
+#if defined(RSGPU_DIAG_CLOCK) && defined(RSGPU_DIAG_VARIANT)
+#define RSGPU_JIT_DIAG_VAR RSGPU_DIAG_VARIANT
+#else
+#define RSGPU_JIT_DIAG_VAR 0
+#endif
+
 namespace rsgpu {
 namespace jit {
 
@@ -274,11 +282,12 @@ struct Wide {
     RJ_HD static constexpr uint32_t pre_u32(int t, int i)
     {
         if (i < 4) {
-            const uint64_t d = enc_ds_read_b128(i < 2 ? PL : PL + 4, ADDR, t * LDS_SRC + (i < 2 ? 0 : LDS_HALF));
+            constexpr int PLD = RSGPU_JIT_DIAG_VAR == 3 ? CL : PL;
+            const uint64_t d = enc_ds_read_b128(i < 2 ? PLD : PLD + 4, ADDR, t * LDS_SRC + (i < 2 ? 0 : LDS_HALF));
             return (i & 1) ? (uint32_t)(d >> 32) : (uint32_t)d;
         }
         if (i == 4)
-            return enc_waitcnt_lgkm(0);
+            return RSGPU_JIT_DIAG_VAR == 4 ? S_NOP0 : enc_waitcnt_lgkm(0);
         const int j = i - 5;
         if (j >= 22)
             return S_NOP0;

@@ -291,12 +291,14 @@ __global__ __launch_bounds__(64 * NV * TPW) __attribute__((amdgpu_num_vgpr(40)))
         return;
     const int k = a.k;
     const int nch = (k + CS - 1) / CS;
-    const uint8_t* const* srcs = a.srcs + (size_t)b * k;
-    uint8_t* const* dsts = a.dsts + (size_t)b * a.dst_stride;
+    // diagnostic variant 1 (diag_clock.h): rows of blocks 0 and 1, 16 KB each
+    const int bw = RSGPU_DIAG_VAR == 1 ? (b & 1) : b;
+    const uint8_t* const* srcs = a.srcs + (size_t)bw * k;
+    uint8_t* const* dsts = a.dsts + (size_t)bw * a.dst_stride;
     const uint8_t* code = a.code + (size_t)b * a.block_stride + (size_t)wave * nch * a.chunk_stride;
     const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint4*)&lds[0][tw][0];
     constexpr uint32_t kBuf = TPW * CS * 2 * 64 * 16;  // bytes between the two chunk buffers
-    const long long off = tile * 2048 + lane * 32;
+    const long long off = (RSGPU_DIAG_VAR == 1 ? (tile & 7) : tile) * 2048 + lane * 32;
     const uint32_t loff = off + 32 <= a.len ? (uint32_t)off : 0u;  // tiles past the row re-read its head
     if (wv == 0)
         asm volatile("s_icache_inv\n s_nop 15\n s_nop 15" ::: "memory");
@@ -356,10 +358,17 @@ __global__ __launch_bounds__(64 * NV * TPW) __attribute__((amdgpu_num_vgpr(40)))
         wait_vm(0);
         {
             const uint32_t m4 = vconst(0x0F0F0F0Fu), m2 = vconst(0x33333333u), m1 = vconst(0x55555555u);
-            for (int t = wave; t < nt; t += NV) {
+            for (int t = wave; t < nt && RSGPU_DIAG_VAR != 5; t += NV) {
                 uint4 u = buf[(t * 2 + 0) * 64 + lane], v = buf[(t * 2 + 1) * 64 + lane];
                 uint32_t Wd[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
                 tr8(Wd, m4, m2, m1);
+                if constexpr (RSGPU_DIAG_VAR == 2) {  // zero planes, the transpose kept
+                    asm volatile("" ::"v"(Wd[0]), "v"(Wd[1]), "v"(Wd[2]), "v"(Wd[3]), "v"(Wd[4]), "v"(Wd[5]),
+                                 "v"(Wd[6]), "v"(Wd[7]));
+#pragma unroll
+                    for (int i = 0; i < 8; ++i)
+                        Wd[i] = 0;
+                }
                 buf[(t * 2 + 0) * 64 + lane] = make_uint4(Wd[0], Wd[1], Wd[2], Wd[3]);
                 buf[(t * 2 + 1) * 64 + lane] = make_uint4(Wd[4], Wd[5], Wd[6], Wd[7]);
             }
@@ -370,7 +379,14 @@ __global__ __launch_bounds__(64 * NV * TPW) __attribute__((amdgpu_num_vgpr(40)))
         ptrs(min(ch + 2, nch - 1), pn);  // in flight during this chunk's code
         const uint32_t la = lds0 + (uint32_t)((ch & 1) * kBuf) + lane * 16;
         const uint8_t* fn = code + (size_t)ch * a.chunk_stride;
-        if constexpr (R == 16)
+        if constexpr (RSGPU_DIAG_VAR == 3 && R == 16)  // zero planes; the LDS reads land in v18..v25
+            asm volatile("v_mov_b32 v10, 0\n v_mov_b32 v11, 0\n v_mov_b32 v12, 0\n v_mov_b32 v13, 0\n"
+                         " v_mov_b32 v14, 0\n v_mov_b32 v15, 0\n v_mov_b32 v16, 0\n v_mov_b32 v17, 0\n"
+                         " s_swappc_b64 s[82:83], %[fn]"
+                         :
+                         : [fn] "s"(fn), "{v9}"(la)
+                         : RSGPU_JW_CALL_CLOBBERS, "s82", "s83", "scc", "memory", RSGPU_J16_ACC_CLOBBERS);
+        else if constexpr (R == 16)
             asm volatile("s_swappc_b64 s[82:83], %[fn]"
                          :
                          : [fn] "s"(fn), "{v9}"(la)

@@ -296,15 +296,9 @@ const rsgpu_ctx::SharedProg* shared_program(rsgpu_ctx* ctx, const uint8_t* coef,
     std::vector<uint8_t> code;
     std::vector<std::pair<size_t, int>> passes;
     if (wide) {
-        for (int p = 0; p < jit::wide_passes(rows); ++p) {
-            const int r0 = jit::wide_pass_row0(rows, p), pr = jit::wide_pass_rows(rows, p);
-            const std::vector<uint8_t> c =
-                jit::build_matrix_code_wide(coef + (size_t)r0 * k, k, pr, jitw_rows(pr), jitw_cs(pr), &stride);
-            if (c.empty())
-                return err(RSGPU_ERR_UNSUPPORTED, "shared program: rows exceed the layout");
-            passes.push_back({code.size(), stride});
-            code.insert(code.end(), c.begin(), c.end());
-        }
+        code = jit::build_matrix_code_wide_passes(coef, k, rows, &passes);
+        if (code.empty())
+            return err(RSGPU_ERR_UNSUPPORTED, "shared program: rows exceed the layout");
     } else {
         code = jit::build_matrix_code(coef, k, rows, &stride);
     }

@@ -157,16 +157,26 @@ long long rsgpu_internal_jitw_emit(int k, int e, const unsigned char* coef, unsi
 }
 
 // Test hook (not in include/rsgpu.h): the host-built shared program of an
-// e x k matrix in the two- or four-wave layout (16 < e <= 64), for the CPU suite to
-// disassemble and interpret.  Returns the bytes needed, or -1; writes only
-// when out_bytes is large enough; *chunk_stride gets the stride.
+// e x k matrix in the two- or four-wave layout (16 < e <= 125; passes of <= 64
+// rows above 64), built exactly as shared_program builds it, for the CPU suite
+// to disassemble and interpret.  Returns the bytes needed, or -1; writes only
+// when out_bytes is large enough; pass p's byte offset and chunk stride go to
+// pass_off[p] / pass_stride[p] (p < max_passes), *npasses gets the count.
 long long rsgpu_internal_jitw_matrix_code(int k, int e, const unsigned char* coef, unsigned char* out,
-                                          size_t out_bytes, int* chunk_stride, int max_ops)
+                                          size_t out_bytes, long long* pass_off, int* pass_stride, int max_passes,
+                                          int* npasses, int max_ops)
 {
-    if (k <= 0 || k + e > 250 || !jitw_rows(e) || !coef || !chunk_stride)
+    if (k <= 0 || k + e > 250 || !jitw_layout(e) || !coef || !pass_off || !pass_stride || !npasses)
         return -1;
-    const std::vector<uint8_t> code =
-        jit::build_matrix_code_wide(coef, k, e, jitw_rows(e), jitw_cs(e), chunk_stride, max_ops);
+    std::vector<std::pair<size_t, int>> passes;
+    const std::vector<uint8_t> code = jit::build_matrix_code_wide_passes(coef, k, e, &passes, max_ops);
+    if (code.empty() || (int)passes.size() > max_passes)
+        return -1;
+    *npasses = (int)passes.size();
+    for (size_t p = 0; p < passes.size(); ++p) {
+        pass_off[p] = (long long)passes[p].first;
+        pass_stride[p] = passes[p].second;
+    }
     if (out && out_bytes >= code.size())
         std::memcpy(out, code.data(), code.size());
     return (long long)code.size();

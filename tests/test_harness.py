@@ -99,3 +99,29 @@ def test_every_timed_kernel_has_algorithmic_bytes():
     priced = bench.alg_bytes(16, 4, 1000)
     missing = sorted(n for n in names if priced.get(n, 0.0) <= 0.0)
     assert not missing, missing
+
+
+@pytest.mark.skipif(not os.path.exists(os.path.join(ROOT, "oracle", "_ref", "libisal_ref.so")),
+                    reason="oracle/_ref not built")
+def test_bench_c1_cpu_line():
+    """bench.py --config c1: BASELINE configs[0], the reference's CPU path at
+    (16, 8, 64000) with the harness accounting (throughput_benchmark.hpp:37-67),
+    host only -- the line must come out without a GPU and without loading
+    the engine."""
+    import json
+    import sys
+    env = dict(os.environ, HIP_VISIBLE_DEVICES="")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--config", "c1", "--c1-seconds", "0.05",
+                        "--cpu-threads", "2"], capture_output=True, text=True, env=env, timeout=300)
+    assert r.returncode == 0, r.stderr
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["device"] == "cpu" and line["n_gpus"] == 0 and line["verified"]
+    assert line["config"]["symbols"] == 16 and line["config"]["symbol_size"] == 64000
+    assert line["config"]["erased"] == 8
+    kinds = [(lg["kind"], lg["threads"]) for lg in line["legs"]]
+    assert kinds == [("reference", 1), ("port", 1), ("reference", 2), ("port", 2)]
+    for lg in line["legs"]:
+        assert lg["failures"] == 0 and lg["encoder_goodput_MBps"] > 0 and lg["decoder_goodput_MBps"] > 0
+    assert line["value"] == round(line["legs"][0]["goodput_GiBps"], 4) > 0
+    assert line["cpu_baseline"]["kind"] == "reference" and line["cpu_baseline"]["cores"] == 1
+    assert "rsgpu" not in r.stderr

@@ -257,42 +257,71 @@ def wide_row0(e, w):
 
 
 def matrix_code_wide(k, e, coef, max_ops=22):
+    """The shared program as rsgpu_capi.cpp shared_program builds it: the
+    code and its passes [(byte offset, chunk stride)] (one pass up to 64
+    rows, passes of <= 64 rows above)."""
     import rsgpu
     f = rsgpu.testhooks().rsgpu_internal_jitw_matrix_code
     f.restype = C.c_longlong
-    f.argtypes = [C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_size_t, C.POINTER(C.c_int), C.c_int]
+    f.argtypes = [C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_size_t, C.POINTER(C.c_longlong),
+                  C.POINTER(C.c_int), C.c_int, C.POINTER(C.c_int), C.c_int]
     coef = np.ascontiguousarray(coef, np.uint8)
-    stride = C.c_int()
-    need = f(k, e, coef.ctypes.data, None, 0, C.byref(stride), max_ops)
+    offs, strides, n = (C.c_longlong * 4)(), (C.c_int * 4)(), C.c_int()
+    need = f(k, e, coef.ctypes.data, None, 0, offs, strides, 4, C.byref(n), max_ops)
+    assert need > 0
     out = np.zeros(need, np.uint8)
-    assert f(k, e, coef.ctypes.data, out.ctypes.data, need, C.byref(stride), max_ops) == need
-    return out.tobytes(), stride.value
+    assert f(k, e, coef.ctypes.data, out.ctypes.data, need, offs, strides, 4, C.byref(n), max_ops) == need
+    return out.tobytes(), [(offs[p], strides[p]) for p in range(n.value)]
 
 
 @pytest.mark.parametrize("k,e,kind", [(64, 32, "rs"), (100, 20, "rs"), (100, 25, "random"),
                                       (128, 32, "random"), (48, 24, "random"), (17, 17, "random"),
                                       (24, 17, "capped"), (218, 32, "rs"), (100, 50, "rs"),
-                                      (128, 64, "random"), (60, 40, "random"), (40, 33, "capped")])
+                                      (128, 64, "random"), (60, 40, "random"), (40, 33, "capped"),
+                                      (150, 100, "random"), (125, 125, "random"), (160, 65, "rs"),
+                                      (90, 70, "capped")])
 def test_shared_matrix_code_wide(k, e, kind):
-    """The GENERATED encode's host-built code for 16 < e <= 64 in the
-    decode's two- / four-wave layout (jit_prog.cpp build_matrix_code_wide: planes
-    v10..v17 from LDS at v9, covered composites from v18, accumulators from
-    v40): interpreted chunk by chunk, every accumulator equals sum_q c[row][q]
-    * src_q over GF(2^8), registers stay in v9..v(40+8R-1), every register is
+    """The GENERATED encode's host-built code for 16 < e <= 125 in the
+    decode's two- / four-wave layout (jit_prog.cpp build_matrix_code_wide_passes,
+    what shared_program runs: planes v10..v17 from LDS at v9, covered
+    composites from v18, accumulators from v40; passes of <= 64 rows above 64,
+    each in the layout of its own rows, at its own offset and chunk stride):
+    interpreted chunk by chunk, every accumulator equals sum_q c[row][q] *
+    src_q over GF(2^8), registers stay in v9..v(40+8R-1), every register is
     read after its LDS load was waited for, and the covers average under the
     22 composites of the full tables."""
-    R, nv = wide_rows(e), wide_waves(e)
-    cs = WIDE[R][0]
     rng = random.Random(k * 1000 + e)
     if kind == "rs":
         coef = rs_rows(k, e)
     else:
         coef = np.array([[rng.randrange(256) for _ in range(k)] for _ in range(e)], np.uint8)
         coef[0, 0] = 0
-    code, stride = matrix_code_wide(k, e, coef, 6 if kind == "capped" else 22)
-    nch = (k + cs - 1) // cs
-    assert stride % 64 == 0 and len(code) == nv * nch * stride
+    code, passes = matrix_code_wide(k, e, coef, 6 if kind == "capped" else 22)
+    npass = (e + 63) // 64 if e > 64 else 1
+    assert len(passes) == npass
     src = [[rng.randrange(256) for _ in range(32)] for _ in range(k)]
+    n_comp = n_src = 0
+    end_of = [o for o, _ in passes[1:]] + [len(code)]
+    for p, (poff, stride) in enumerate(passes):
+        pr0, pr = p * e // npass, (p + 1) * e // npass - p * e // npass  # rs_jit.h wide_pass_row0
+        R, nv = wide_rows(pr), wide_waves(pr)
+        cs = WIDE[R][0]
+        nch = (k + cs - 1) // cs
+        assert stride % 64 == 0 and end_of[p] - poff == nv * nch * stride
+        nc, ns = interpret_wide_pass(code[poff:end_of[p]], stride, k, pr, R, nv, cs, nch,
+                                     coef[pr0:pr0 + pr], src)
+        n_comp += nc
+        n_src += ns
+    # per (wave, source): the capped covers fall back to the full tables
+    if kind == "capped":
+        assert n_comp / n_src > 18, n_comp / n_src
+    else:
+        assert n_comp / n_src < 20, n_comp / n_src
+
+
+def interpret_wide_pass(code, stride, k, e, R, nv, cs, nch, coef, src):
+    """Runs one pass of shared wide code (rows coef[0..e-1]) on the CPU and
+    checks every accumulator; returns (composites, sources) seen."""
     n_comp = n_src = 0
     for w in range(nv):
         nslot = wide_row0(e, w + 1) - wide_row0(e, w)
@@ -325,11 +354,7 @@ def test_shared_matrix_code_wide(k, e, kind):
                 want = [x ^ g.gf_mul(int(coef[row, q]), y) for x, y in zip(want, src[q])]
             got = unplanes([regs[40 + 8 * s + b] for b in range(8)])
             assert got == want, (k, e, row)
-    # per (wave, source): the capped covers fall back to the full tables
-    if kind == "capped":
-        assert n_comp / n_src > 18, n_comp / n_src
-    else:
-        assert n_comp / n_src < 20, n_comp / n_src
+    return n_comp, n_src
 
 
 def emitw(k, e, coef):

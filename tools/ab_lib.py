@@ -11,7 +11,9 @@
                 emission beside the decode (0 / 1 off, -1 the library's choice)
 
 The knobs go through rsgpu_testhooks.cpp (librsgpu_testhooks.so), applied to
-every context bench.py creates; the product library exports none of them."""
+every context bench.py creates; the product library exports none of them.
+They write the context at this tree's layout, so they are refused with
+--lib (another build's rsgpu_ctx may differ)."""
 import argparse
 import ctypes
 import os
@@ -29,6 +31,12 @@ def main() -> int:
     ap.add_argument("--jitw-prefetch", type=int, default=None)
     ap.add_argument("--decode-pipeline", type=int, default=None)
     ab, rest = ap.parse_known_args()
+    has_knobs = any(v is not None for v in (ab.jitw_tiles, ab.jitw_prefetch, ab.decode_pipeline))
+    if ab.lib and has_knobs:
+        # the hooks write rsgpu_ctx fields at the offsets of THIS tree's
+        # rsgpu_ctx.h; another build's context may lay them out differently
+        ap.error("--lib cannot be combined with the layout knobs (the test hooks know only this "
+                 "tree's rsgpu_ctx layout); build the variant with the knob's default instead")
     if ab.lib:
         os.environ["RSGPU_LIB"] = os.path.abspath(ab.lib)
     import rsgpu  # noqa: E402  (reads RSGPU_LIB)
