@@ -25,6 +25,11 @@
 //             registers, the VALU works on zero planes (VALU quiet)
 //   4 nowait  the generated decode's per-source LDS wait removed
 //   5 notr    the source transposes skipped (raw bytes used as planes)
+//   6 phases  the product stream plus s_memtime stamps between the phases of
+//             k_rs_jitw (per-wave cycle sums of one workgroup in kEvery)
+//   7 code0   k_rs_jitw runs block 0's code in every block (L2-resident code)
+//   8 chunk0  k_rs_jitw runs each wave's chunk-0 code for every full chunk
+//             (instruction-cache-resident code)
 #if defined(RSGPU_DIAG_CLOCK) && defined(RSGPU_DIAG_VARIANT)
 #define RSGPU_DIAG_VAR RSGPU_DIAG_VARIANT
 #else
@@ -72,6 +77,42 @@ __device__ __forceinline__ unsigned long long memrealtime()
             s_[3] = r1_;                                                                            \
         }                                                                                           \
     } while (0)
+// variant 6: per-wave cycle sums per phase of the stamped workgroups
+#define RSGPU_DIAG_PHASE_TABLE \
+    static __device__ unsigned long long g_rsgpu_phase[::rsgpu::diag::kSlots][::rsgpu::diag::kPhaseWaves][::rsgpu::diag::kPhases];
+namespace rsgpu {
+namespace diag {
+constexpr int kPhases = 8;
+constexpr int kPhaseWaves = 4;
+struct PhaseTimer {
+    unsigned long long sum[kPhases] = {}, t, start;
+    __device__ PhaseTimer() : t(memtime()), start(t) {}
+    __device__ void mark(int p)
+    {
+        const unsigned long long n = memtime();
+        sum[p] += n - t;
+        t = n;
+    }
+    template <class Table>
+    __device__ void end(Table& tab, int wave)
+    {
+        sum[kPhases - 1] = memtime() - start;
+        const unsigned lin = blockIdx.x + gridDim.x * blockIdx.y;
+        if ((threadIdx.x & 63) == 0 && lin % kEvery == 0 && wave < kPhaseWaves)
+            for (int i = 0; i < kPhases; ++i)
+                tab[(lin / kEvery) % kSlots][wave][i] = sum[i];
+    }
+};
+}  // namespace diag
+}  // namespace rsgpu
+#define RSGPU_DIAG_PHASE_READER(NAME)                                                               \
+    hipError_t NAME(void* host, size_t bytes)                                                       \
+    {                                                                                               \
+        return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_rsgpu_phase),                                 \
+                                   bytes < sizeof(g_rsgpu_phase) ? bytes : sizeof(g_rsgpu_phase), 0, \
+                                   hipMemcpyDeviceToHost);                                          \
+    }
+
 // host side, in the same translation unit as the table
 #define RSGPU_DIAG_READER(NAME)                                                                     \
     hipError_t NAME(void* host, size_t bytes)                                                       \
@@ -88,6 +129,8 @@ __device__ __forceinline__ unsigned long long memrealtime()
     }
 #else
 #define RSGPU_DIAG_TABLE
+#define RSGPU_DIAG_PHASE_TABLE
+#define RSGPU_DIAG_PHASE_READER(NAME)
 #define RSGPU_DIAG_BEGIN()
 #define RSGPU_DIAG_END() \
     do {                 \

@@ -46,6 +46,17 @@ using bs::wait_vm;
 constexpr int C = 8;  // sources per LDS chunk (double-buffered)
 
 RSGPU_DIAG_TABLE
+RSGPU_DIAG_PHASE_TABLE
+
+// phase stamps of the diagnostic variant 6 (diag_clock.h); nothing otherwise
+struct NoPhases {
+    __device__ void mark(int) {}
+};
+#if RSGPU_DIAG_VAR == 6
+using JitwPhases = diag::PhaseTimer;
+#else
+using JitwPhases = NoPhases;
+#endif
 
 // Instrumentation points of k_rs_jit.  The product instantiates JitHooks:
 // no timers, every wave runs its own block's code, wave 0 invalidates the
@@ -295,7 +306,9 @@ __global__ __launch_bounds__(64 * NV * TPW) __attribute__((amdgpu_num_vgpr(40)))
     const int bw = RSGPU_DIAG_VAR == 1 ? (b & 1) : b;
     const uint8_t* const* srcs = a.srcs + (size_t)bw * k;
     uint8_t* const* dsts = a.dsts + (size_t)bw * a.dst_stride;
-    const uint8_t* code = a.code + (size_t)b * a.block_stride + (size_t)wave * nch * a.chunk_stride;
+    // diagnostic variant 7: block 0's code for every block (L2-resident)
+    const uint8_t* code = a.code + (size_t)(RSGPU_DIAG_VAR == 7 ? 0 : b) * a.block_stride +
+                          (size_t)wave * nch * a.chunk_stride;
     const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint4*)&lds[0][tw][0];
     constexpr uint32_t kBuf = TPW * CS * 2 * 64 * 16;  // bytes between the two chunk buffers
     const long long off = (RSGPU_DIAG_VAR == 1 ? (tile & 7) : tile) * 2048 + lane * 32;
@@ -314,9 +327,9 @@ __global__ __launch_bounds__(64 * NV * TPW) __attribute__((amdgpu_num_vgpr(40)))
         for (int i = 0; i < PW; ++i)
             p[i] = csrcs[c0 + min(wave + NV * i, nt - 1)];  // in bounds, unconditional
     };
-    auto issue = [&](int ch, const uint8_t* const (&p)[PW]) {
+    auto issue = [&](int ch, int par, const uint8_t* const (&p)[PW]) {
         const int c0 = ch * CS, nt = min(CS, k - c0);
-        const uint32_t base = lds0 + (uint32_t)((ch & 1) * kBuf);
+        const uint32_t base = lds0 + (uint32_t)(par * kBuf);
 #pragma unroll
         for (int i = 0; i < PW; ++i) {
             const int t = wave + NV * i;
@@ -334,11 +347,33 @@ __global__ __launch_bounds__(64 * NV * TPW) __attribute__((amdgpu_num_vgpr(40)))
         asm volatile(RSGPU_J12_ZERO ::: RSGPU_J12_ACC_CLOBBERS);
     else
         asm volatile(RSGPU_J10_ZERO ::: RSGPU_J10_ACC_CLOBBERS);
+    JitwPhases ph;
+    // The chunks' order is free (each chunk's code only adds into the
+    // accumulators).  A rotation by the time the workgroup starts, chunk
+    // (t / kRot) % nch first, keeps the workgroups that share a CU pair's
+    // instruction cache at about the same chunk of their block's code
+    // (workgroups that start later begin where the others are).
+    // Rounded to the nearest period, so a workgroup starts with the chunk the
+    // others are about to be in (same box x3, profiles/r05_rot/: C3 decode
+    // 22.53-22.58 ms at 600 ticks, 23.04-23.08 in order; 450-800 all gain).
+    int rot = 0;
+    if (a.chunk_rot_ticks > 0) {
+        __shared__ int s_rot;
+        if (threadIdx.x == 0) {
+            unsigned long long t;
+            asm volatile("s_memrealtime %0\n s_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+            const unsigned long long p = (unsigned long long)a.chunk_rot_ticks;
+            s_rot = (int)(((t + p / 2) / p) % (unsigned long long)nch);
+        }
+        __syncthreads();
+        rot = __builtin_amdgcn_readfirstlane(s_rot);
+    }
+    auto chunk_of = [&](int i) { return i + rot >= nch ? i + rot - nch : i + rot; };
     const uint8_t* pc[PW];
     const uint8_t* pn[PW];
-    ptrs(0, pc);
-    issue(0, pc);
-    ptrs(min(1, nch - 1), pn);
+    ptrs(chunk_of(0), pc);
+    issue(chunk_of(0), 0, pc);
+    ptrs(chunk_of(min(1, nch - 1)), pn);
     if (a.code_prefetch) {
         // the block's workgroups split its code (both row halves) and pull
         // it into L2 with vector loads, every line in flight at once, so the
@@ -352,14 +387,16 @@ __global__ __launch_bounds__(64 * NV * TPW) __attribute__((amdgpu_num_vgpr(40)))
             asm volatile("global_load_dword %0, %1, off\n s_waitcnt vmcnt(0)" : "=v"(d) : "v"(cb + (i << 7)) : "memory");
         }
     }
-    for (int ch = 0; ch < nch; ++ch) {
+    for (int i = 0; i < nch; ++i) {
+        const int ch = chunk_of(i), par = i & 1;  // the chunk, its LDS buffer
         const int nt = min(CS, k - ch * CS);
-        uint4* buf = lds[ch & 1][tw];
+        uint4* buf = lds[par][tw];
+        ph.mark(0);  // phase 0: the previous call's return .. here (loop overhead, start)
         wait_vm(0);
+        ph.mark(1);  // phase 1: this chunk's LDS-DMA
         {
-            const uint32_t m4 = vconst(0x0F0F0F0Fu), m2 = vconst(0x33333333u), m1 = vconst(0x55555555u);
-            for (int t = wave; t < nt && RSGPU_DIAG_VAR != 5; t += NV) {
-                uint4 u = buf[(t * 2 + 0) * 64 + lane], v = buf[(t * 2 + 1) * 64 + lane];
+            auto transpose = [&](int t, uint4 u, uint4 v) {
+                const uint32_t m4 = vconst(0x0F0F0F0Fu), m2 = vconst(0x33333333u), m1 = vconst(0x55555555u);
                 uint32_t Wd[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
                 tr8(Wd, m4, m2, m1);
                 if constexpr (RSGPU_DIAG_VAR == 2) {  // zero planes, the transpose kept
@@ -371,14 +408,49 @@ __global__ __launch_bounds__(64 * NV * TPW) __attribute__((amdgpu_num_vgpr(40)))
                 }
                 buf[(t * 2 + 0) * 64 + lane] = make_uint4(Wd[0], Wd[1], Wd[2], Wd[3]);
                 buf[(t * 2 + 1) * 64 + lane] = make_uint4(Wd[4], Wd[5], Wd[6], Wd[7]);
+            };
+#ifndef RSGPU_JW_TR_BATCH
+#define RSGPU_JW_TR_BATCH 1
+#endif
+            if constexpr (RSGPU_JW_TR_BATCH && RSGPU_DIAG_VAR != 5 && RSGPU_DIAG_VAR != 2 && PW <= 3) {
+                // the wave's share (t = wave + NV i) in hand-allocated
+                // registers (gen_tc_handlers.py jw_transposes): the first two
+                // sources read together, the third while the second is
+                // transposed, so the chunk exposes one LDS latency instead of
+                // one per source (the compiler's 40 VGPRs spill doing this)
+                const uint32_t ta = lds0 + (uint32_t)(par * kBuf) + (uint32_t)wave * 2048 + lane * 16;
+                const int n = (wave < nt) + (wave + NV < nt) + (PW > 2 && wave + 2 * NV < nt);
+#define RSGPU_JW_TR(N, V) asm volatile(RSGPU_JW_TR##N##_NV##V ::"v"(ta) : RSGPU_JW_TR_CLOBBERS, "memory")
+                if constexpr (NV == 2) {
+                    if (n == 3)
+                        RSGPU_JW_TR(3, 2);
+                    else if (n == 2)
+                        RSGPU_JW_TR(2, 2);
+                    else if (n == 1)
+                        RSGPU_JW_TR(1, 2);
+                } else {
+                    if (n == 2)
+                        RSGPU_JW_TR(2, 4);
+                    else if (n == 1)
+                        RSGPU_JW_TR(1, 4);
+                }
+#undef RSGPU_JW_TR
+            } else {
+                for (int t = wave; t < nt && RSGPU_DIAG_VAR != 5; t += NV)
+                    transpose(t, buf[(t * 2 + 0) * 64 + lane], buf[(t * 2 + 1) * 64 + lane]);
             }
         }
+        ph.mark(2);  // phase 2: transposes
         barrier_lds();
-        if (ch + 1 < nch)
-            issue(ch + 1, pn);
-        ptrs(min(ch + 2, nch - 1), pn);  // in flight during this chunk's code
-        const uint32_t la = lds0 + (uint32_t)((ch & 1) * kBuf) + lane * 16;
-        const uint8_t* fn = code + (size_t)ch * a.chunk_stride;
+        ph.mark(3);  // phase 3: the chunk barrier
+        if (i + 1 < nch)
+            issue(chunk_of(i + 1), par ^ 1, pn);
+        ptrs(chunk_of(min(i + 2, nch - 1)), pn);  // in flight during this chunk's code
+        ph.mark(4);  // phase 4: next chunk's LDS-DMA issue, row pointers
+        const uint32_t la = lds0 + (uint32_t)(par * kBuf) + lane * 16;
+        // diagnostic variant 8: chunk 0's code for every full chunk (the
+        // wave's code stays in the instruction cache)
+        const uint8_t* fn = code + (size_t)(RSGPU_DIAG_VAR == 8 && nt == CS ? 0 : ch) * a.chunk_stride;
         if constexpr (RSGPU_DIAG_VAR == 3 && R == 16)  // zero planes; the LDS reads land in v18..v25
             asm volatile("v_mov_b32 v10, 0\n v_mov_b32 v11, 0\n v_mov_b32 v12, 0\n v_mov_b32 v13, 0\n"
                          " v_mov_b32 v14, 0\n v_mov_b32 v15, 0\n v_mov_b32 v16, 0\n v_mov_b32 v17, 0\n"
@@ -401,6 +473,7 @@ __global__ __launch_bounds__(64 * NV * TPW) __attribute__((amdgpu_num_vgpr(40)))
                          :
                          : [fn] "s"(fn), "{v9}"(la)
                          : RSGPU_JW_CALL_CLOBBERS, "s82", "s83", "scc", "memory", RSGPU_J10_ACC_CLOBBERS);
+        ph.mark(5);  // phase 5: the generated code
     }
     // the output pointers likewise: all R loads under one wait
     typedef uint8_t* const __attribute__((address_space(4)))* CDsts;
@@ -424,6 +497,10 @@ __global__ __launch_bounds__(64 * NV * TPW) __attribute__((amdgpu_num_vgpr(40)))
                 ...);
         }(std::make_integer_sequence<int, R>{});
     }
+    ph.mark(6);  // phase 6: output transposes and stores
+#if RSGPU_DIAG_VAR == 6
+    ph.end(g_rsgpu_phase, wv);
+#endif
     RSGPU_DIAG_END();
 }
 
@@ -438,6 +515,7 @@ __global__ void k_jit_fill(uint64_t* code, long long n)
 }
 
 RSGPU_DIAG_READER(diag_read_jitw)
+RSGPU_DIAG_PHASE_READER(diag_read_jitw_phase)
 
 }  // namespace jitk
 
@@ -597,6 +675,14 @@ int jitw_rows(int e)
     return e > 24 ? 16 : e > 20 ? 12 : e > 16 ? 10 : 0;
 }
 
+int jitw_rot_ticks(int rows)
+{
+    // one chunk's work per wave, CS (8 R + 24) VALU, scaled from C3's
+    // measured optimum (R 16, CS 6: 600 ticks)
+    const int r = jitw_rows(rows), cs = jitw_cs(rows);
+    return r ? 600 * cs * (8 * r + 24) / (6 * (8 * 16 + 24)) : 0;
+}
+
 int jitw_cs(int e) { return jitw_rows(e) == 16 ? jit::J16::CS : jitw_rows(e) == 12 ? jit::J12::CS : jit::J10::CS; }
 
 size_t jitw_chunk_stride(int e)
@@ -606,8 +692,15 @@ size_t jitw_chunk_stride(int e)
 }
 
 // the layout covers e: 16 < e <= 64 in one launch, 64 < e <= 125 in passes
-bool jitw_layout(int e) { return e > 16 && (e <= 64 || (e <= 128 && jitw_rows(jit::wide_pass_rows(e, 0)) &&
-                                                        jitw_rows(jit::wide_pass_rows(e, jit::wide_passes(e) - 1)))); }
+bool jitw_layout(int e)
+{
+#ifdef RSGPU_AB_JIT8  // A/B build only: the 4 x 8-row layout for e <= 32
+    if (e <= 32)
+        return false;
+#endif
+    return e > 16 && (e <= 64 || (e <= 128 && jitw_rows(jit::wide_pass_rows(e, 0)) &&
+                                                        jitw_rows(jit::wide_pass_rows(e, jit::wide_passes(e) - 1))));
+}
 
 // one block's code of a pass of `rows` (<= 64) rows
 size_t jitw_pass_bytes(int k, int rows)

@@ -117,7 +117,12 @@ struct JitArgs {
     int xcd_order;                   // non-zero: XCD-contiguous (block, tile) order
     int tiles_per_wg = 1;            // k_rs_jitw: column tiles per workgroup (1, 2 or 3)
     int code_prefetch = 0;           // k_rs_jitw: workgroups pull their block's code into L2 first
+    int chunk_rot_ticks = 0;         // k_rs_jitw: > 0 rotates the chunk order by the start time
+                                     // (s_memrealtime / chunk_rot_ticks), 0 = chunks in order
 };
+// k_rs_jitw's chunk rotation period for `rows` rows at k sources: about one
+// chunk's duration in 100 MHz ticks (measured best at 600 for C3's 16 rows)
+int jitw_rot_ticks(int rows);
 size_t jit_code_bytes(int k, int e, long long blocks);
 // k_rs_jit's straight-line code (rs_jit.h) for every (block, wave, chunk) at
 // code + ((b NW + w) nch + ch) jit::chunk_stride(8), from the decode rows

@@ -1224,6 +1224,10 @@ int jitw_launch(rsgpu_ctx* ctx, int k, int e, size_t len, size_t blocks, const u
             const long long lines = (long long)jitw_pass_bytes(k, rows) / 128;
             j.code_prefetch = ctx->jitw_prefetch >= 0 ? ctx->jitw_prefetch : lines >= 32 * wgs;
         }
+        // chunk order rotated by each workgroup's start time, so the
+        // workgroups sharing a CU pair's instruction cache walk their block's
+        // code in step (k_rs_jitw)
+        j.chunk_rot_ticks = ctx->jitw_rot >= 0 ? ctx->jitw_rot : jitw_rot_ticks(rows);
         const int r = jitw_rows(rows);
         KTimer kt(ctx,
                   e > 64  ? "k_rs_jitw_passes(decode)"

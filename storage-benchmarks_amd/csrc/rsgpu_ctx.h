@@ -27,6 +27,7 @@ struct rsgpu_ctx {
     int decode_kernel = RSGPU_DECODE_AUTO;
     int jitw_tpw = 0;  // k_rs_jitw column tiles per workgroup (0: by geometry)
     int jitw_prefetch = -1;  // k_rs_jitw code prefetch into L2 (-1: by geometry)
+    int jitw_rot = -1;       // k_rs_jitw chunk rotation period, ticks (-1: by geometry, 0: off)
     // short-row generated decode: prepare + emission on `aux` beside the
     // decode, in decode_pipe slices (-1: by geometry, 0 / 1: off)
     int decode_pipe = -1;

@@ -20,6 +20,7 @@ hipError_t diag_read_bs_clear();
 namespace jitk {
 hipError_t diag_read_jitw(void* host, size_t bytes);
 hipError_t diag_read_jitw_clear();
+hipError_t diag_read_jitw_phase(void* host, size_t bytes);
 }  // namespace jitk
 }  // namespace rsgpu
 
@@ -41,5 +42,12 @@ int rsgpu_diag_clock_clear(void)
 }
 
 int rsgpu_diag_clock_slots(void) { return rsgpu::diag::kSlots; }
+
+// variant 6 only: k_rs_jitw's per-wave phase cycle sums,
+// [kSlots][kPhaseWaves][kPhases] (diag_clock.h); zeros in other builds
+int rsgpu_diag_phase_read(unsigned long long* out, size_t bytes)
+{
+    return rsgpu::jitk::diag_read_jitw_phase(out, bytes) == hipSuccess ? 0 : -2;
+}
 
 }  // extern "C"

@@ -71,6 +71,16 @@ int rsgpu_internal_set_jitw_prefetch(rsgpu_ctx* ctx, int n)
     return RSGPU_OK;
 }
 
+// A-B hook (not part of include/rsgpu.h): k_rs_jitw's chunk rotation period
+// in 100 MHz ticks (0 chunks in order, -1 the library's choice).
+int rsgpu_internal_set_jitw_rot(rsgpu_ctx* ctx, int n)
+{
+    if (!ctx || n < -1 || n > 1000000)
+        return RSGPU_ERR_ARG;
+    ctx->jitw_rot = n;
+    return RSGPU_OK;
+}
+
 // Test / A-B hook (not part of include/rsgpu.h): slices of the short-row
 // generated decode whose prepare and emission run beside the decode
 // (rsgpu_decode_blocks; 0 or 1 off, -1 the library's choice).

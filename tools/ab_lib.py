@@ -9,11 +9,14 @@
 --jitw-prefetch its code prefetch into L2 (0 off, 1 on, -1 the library's choice)
 --decode-pipeline  slices of the short-row generated decode with prepare and
                 emission beside the decode (0 / 1 off, -1 the library's choice)
+--jitw-rot      its chunk rotation period in 100 MHz ticks (0 in order, -1 the
+                library's choice)
 
 The knobs go through rsgpu_testhooks.cpp (librsgpu_testhooks.so), applied to
 every context bench.py creates; the product library exports none of them.
-They write the context at this tree's layout, so they are refused with
---lib (another build's rsgpu_ctx may differ)."""
+They write the context at this tree's layout, so they are refused with a
+--lib other than this tree's own librsgpu.so (another build's rsgpu_ctx may
+differ)."""
 import argparse
 import ctypes
 import os
@@ -30,9 +33,11 @@ def main() -> int:
     ap.add_argument("--jitw-tiles", type=int, default=None)
     ap.add_argument("--jitw-prefetch", type=int, default=None)
     ap.add_argument("--decode-pipeline", type=int, default=None)
+    ap.add_argument("--jitw-rot", type=int, default=None)
     ab, rest = ap.parse_known_args()
-    has_knobs = any(v is not None for v in (ab.jitw_tiles, ab.jitw_prefetch, ab.decode_pipeline))
-    if ab.lib and has_knobs:
+    has_knobs = any(v is not None for v in (ab.jitw_tiles, ab.jitw_prefetch, ab.decode_pipeline, ab.jitw_rot))
+    own = os.path.join(ROOT, "storage-benchmarks_amd", "rsgpu", "librsgpu.so")
+    if ab.lib and has_knobs and os.path.realpath(ab.lib) != os.path.realpath(own):
         # the hooks write rsgpu_ctx fields at the offsets of THIS tree's
         # rsgpu_ctx.h; another build's context may lay them out differently
         ap.error("--lib cannot be combined with the layout knobs (the test hooks know only this "
@@ -49,6 +54,8 @@ def main() -> int:
         knobs.append(("rsgpu_internal_set_jitw_prefetch", ab.jitw_prefetch))
     if ab.decode_pipeline is not None:
         knobs.append(("rsgpu_internal_set_decode_pipeline", ab.decode_pipeline))
+    if ab.jitw_rot is not None:
+        knobs.append(("rsgpu_internal_set_jitw_rot", ab.jitw_rot))
     if knobs:
         init = rsgpu.Context.__init__
 

@@ -143,6 +143,18 @@ def main() -> int:
                                            round(float(np.percentile(clk, 90)), 1)]
                 ph["wg_life_us_median"] = round(float(np.median(life)), 2)
                 ph["stamped_wgs"] = int(ok.sum())
+            if kind == "dec" and hasattr(lib, "rsgpu_diag_phase_read"):
+                # variant 6 builds: k_rs_jitw's per-wave cycles per phase
+                lib.rsgpu_diag_phase_read.argtypes = [C.c_void_p, C.c_size_t]
+                pt = np.zeros((slots, 4, 8), np.uint64)
+                assert lib.rsgpu_diag_phase_read(pt.ctypes.data, pt.nbytes) == 0
+                pt = pt.astype(np.float64)
+                live = pt[:, :, 7] > 0
+                if live.any():
+                    names = ["loop", "wait_dma", "transpose", "barrier", "issue_ptrs", "code", "store", "life"]
+                    mean = pt[live].mean(axis=0)
+                    ph["phase_cycles_per_wave"] = {n: round(float(v), 0) for n, v in zip(names, mean)}
+                    ph["phase_frac"] = {n: round(float(v / mean[7]), 4) for n, v in zip(names[:7], mean[:7])}
         phases.append(ph)
         print(json.dumps(ph), flush=True)
 
