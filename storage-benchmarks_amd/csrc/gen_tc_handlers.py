@@ -226,107 +226,6 @@ def tables() -> list:
     return ins
 
 
-def tr8_asm(b: int, m4: int, m2: int, m1: int) -> list:
-    """bitslice.h tr8 on v[b..b+7] (W0..W7) with v[b+8..b+11] as temporaries,
-    written so that every 64-bit shift reads an even-aligned register pair
-    and no move is needed: W0..W3 end in v[b+2..b+5], W4..W7 in
-    v[b+6..b+9] (two ds_write_b128 quads).  24 v_bitop3 + 12 64-bit shifts,
-    as the compiler's form; each v_bitop3 f(a, c, m) = (a & m) | (c & ~m)."""
-    R = [b + i for i in range(8)]
-    T = [b + 8 + i for i in range(4)]
-    out = []
-
-    def shr(d, s, src):
-        out.append(f"v_lshrrev_b64 v[{d}:{d + 1}], {s}, v[{src}:{src + 1}]")
-
-    def shl(d, s, src):
-        out.append(f"v_lshlrev_b64 v[{d}:{d + 1}], {s}, v[{src}:{src + 1}]")
-
-    def f(d, a, c, m):
-        out.append(f"v_bitop3_b32 v{d}, v{a}, v{c}, v{m} bitop3:0xe4")
-
-    def nop():
-        out.append("s_nop 0")
-
-    # stage 1 (4-bit blocks), in place: (W0, W1 | W4, W5), (W2, W3 | W6, W7)
-    for lo, hi in ((0, 4), (2, 6)):
-        shr(T[0], 4, R[lo])
-        shl(T[2], 4, R[hi])
-        nop()
-        f(R[lo], R[lo], T[2], m4)
-        f(R[lo + 1], R[lo + 1], T[3], m4)
-        f(R[hi], T[0], R[hi], m4)
-        f(R[hi + 1], T[1], R[hi + 1], m4)
-    # stage 2 (2-bit blocks): outputs paired for stage 3, (W0, W2) (W1, W3) ...
-    shr(T[0], 2, R[0])
-    shl(T[2], 2, R[2])
-    nop()
-    f(R[3], T[1], R[3], m2)      # W3
-    f(T[1], T[0], R[2], m2)      # W2
-    f(T[0], R[0], T[2], m2)      # W0
-    f(R[2], R[1], T[3], m2)      # W1  -> (W0, W2) = T0:T1, (W1, W3) = R2:R3
-    shr(R[0], 2, R[4])
-    shl(T[2], 2, R[6])
-    nop()
-    f(R[7], R[1], R[7], m2)      # W7
-    f(R[1], R[0], R[6], m2)      # W6
-    f(R[0], R[4], T[2], m2)      # W4
-    f(R[6], R[5], T[3], m2)      # W5  -> (W4, W6) = R0:R1, (W5, W7) = R6:R7
-    # stage 3 (1-bit blocks): results as two quads
-    shr(R[4], 1, T[0])
-    shl(T[2], 1, R[2])
-    nop()
-    f(R[5], R[5], R[3], m1)      # W3
-    f(R[3], R[4], R[2], m1)      # W1
-    f(R[2], T[0], T[2], m1)      # W0
-    f(R[4], T[1], T[3], m1)      # W2  -> W0..W3 = v[b+2..b+5]
-    shr(T[0], 1, R[0])
-    shl(T[2], 1, R[6])
-    nop()
-    f(T[1], T[1], R[7], m1)      # W7
-    f(R[7], T[0], R[6], m1)      # W5
-    f(R[6], R[0], T[2], m1)      # W4
-    f(T[0], R[1], T[3], m1)      # W6  -> W4..W7 = v[b+6..b+9]
-    return out
-
-
-def jw_transposes(n: int, stride: int) -> list:
-    """k_rs_jitw's per-chunk source transposes of one wave, in place in LDS:
-    n <= 3 sources at %0, %0 + stride, %0 + 2 stride (bytes 0-15 of a lane at
-    +0, 16-31 at +1024).  The first two are read together, the third while
-    the second is transposed: one exposed LDS latency per chunk, not one per
-    source.  Registers v10..v36 (free between the generated-code calls)."""
-    A, B, MK = 10, 22, (34, 35, 36)
-    out = [f"v_mov_b32 v{MK[0]}, 0x0f0f0f0f", f"v_mov_b32 v{MK[1]}, 0x33333333",
-           f"v_mov_b32 v{MK[2]}, 0x55555555"]
-
-    def rd(base, off):
-        out.append(f"ds_read_b128 v[{base}:{base + 3}], %0 offset:{off}")
-        out.append(f"ds_read_b128 v[{base + 4}:{base + 7}], %0 offset:{off + 1024}")
-
-    def wr(base, off):  # tr8 leaves the quads at base + 2 and base + 6
-        out.append(f"ds_write_b128 %0, v[{base + 2}:{base + 5}] offset:{off}")
-        out.append(f"ds_write_b128 %0, v[{base + 6}:{base + 9}] offset:{off + 1024}")
-
-    rd(A, 0)
-    if n >= 2:
-        rd(B, stride)
-    out.append(f"s_waitcnt lgkmcnt({2 if n >= 2 else 0})")
-    out += tr8_asm(A, *MK)
-    wr(A, 0)
-    if n >= 2:
-        if n == 3:
-            rd(A, 2 * stride)  # the write above read its registers at issue
-        out.append(f"s_waitcnt lgkmcnt({4 if n == 3 else 2})")  # B's reads (in order)
-        out += tr8_asm(B, *MK)
-        wr(B, stride)
-    if n == 3:
-        out.append("s_waitcnt lgkmcnt(2)")  # C's reads
-        out += tr8_asm(A, *MK)
-        wr(A, 2 * stride)
-    return out
-
-
 def main() -> None:
     out = sys.argv[1]
     lines = [
@@ -387,13 +286,6 @@ def main() -> None:
                        for q in range(4))
         lines.append(f'#define RSGPU_JW_READ_SLOT64_{slot} "{body}"')
     lines.append("#define RSGPU_JW_CALL_CLOBBERS " + ", ".join(f'"v{r}"' for r in range(10, 40)))
-    for nv in (2, 4):
-        for n in (1, 2, 3):
-            lines.append(f"#define RSGPU_JW_TR{n}_NV{nv} \\")
-            for i in jw_transposes(n, nv * 2048):
-                lines.append(f'    "{i}\\n" \\')
-            lines.append("")
-    lines.append("#define RSGPU_JW_TR_CLOBBERS " + ", ".join(f'"v{r}"' for r in range(10, 37)))
     vclob = sorted(set(range(STAGE, STAGE + 8)) | set(TABLE_REGS))
     sclob = list(range(BANK[0], BANK[0] + 16)) + [SM0, RET, RET + 1] + list(range(BANK[1], BANK[1] + 16))
     for ra in RA_LIST:

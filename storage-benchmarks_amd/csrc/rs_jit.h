@@ -235,7 +235,9 @@ template <int R_, int CS_>
 struct Wide {
     static constexpr int R = R_, CS = CS_;
     static constexpr int ADDR = 9, PL = 10, CL = 18, ACC = 40;
-    static constexpr int PRE = 112;  // bytes per source before the multiply-accumulates
+    // bytes per source before the multiply-accumulates (diagnostic variants
+    // 9 / 10 add two LDS reads / eight VALU per source: marginal prices)
+    static constexpr int PRE = 112 + (RSGPU_JIT_DIAG_VAR == 9 ? 16 : RSGPU_JIT_DIAG_VAR == 10 ? 32 : 0);
     RJ_HD static constexpr int src_bytes(int nslot) { return PRE + 64 * nslot; }
     RJ_HD static constexpr int chunk_stride() { return (CS * src_bytes(R) + 8 + 63) / 64 * 64; }
 
@@ -281,6 +283,20 @@ struct Wide {
     // 32-bit word i (< PRE / 4 = 28) of source t's preamble
     RJ_HD static constexpr uint32_t pre_u32(int t, int i)
     {
+        if constexpr (RSGPU_JIT_DIAG_VAR == 9) {  // the planes read a second time, into v18..v25
+            if (i >= 4 && i < 8) {
+                const uint64_t d = enc_ds_read_b128(i < 6 ? CL : CL + 4, ADDR, t * LDS_SRC + (i < 6 ? 0 : LDS_HALF));
+                return (i & 1) ? (uint32_t)(d >> 32) : (uint32_t)d;
+            }
+            if (i >= 8)
+                i -= 4;
+        }
+        if constexpr (RSGPU_JIT_DIAG_VAR == 10) {  // after the composites: v18..v21 ^= v10 twice
+            if (i >= 27 && i < 35)
+                return enc_xor_e32(CL + ((i - 27) >> 1), PL, CL + ((i - 27) >> 1));
+            if (i >= 35)
+                return S_NOP0;
+        }
         if (i < 4) {
             constexpr int PLD = RSGPU_JIT_DIAG_VAR == 3 ? CL : PL;
             const uint64_t d = enc_ds_read_b128(i < 2 ? PLD : PLD + 4, ADDR, t * LDS_SRC + (i < 2 ? 0 : LDS_HALF));
@@ -330,8 +346,9 @@ using J10 = Wide<10, 5>;
 // coefficient c for output plane b at [8 c + b], and the 14 preamble words
 // of chunk position t at [14 t + i / 2] (i = 0 .. 27 as pre_u32).
 struct WideTables {
+    static constexpr int PW = Wide<16, 6>::PRE / 8;  // preamble words per source (14)
     uint64_t mac[256 * 8];
-    uint64_t pre[6 * 14];
+    uint64_t pre[6 * PW];
 };
 RJ_HD constexpr WideTables wide_tables()
 {
@@ -340,8 +357,8 @@ RJ_HD constexpr WideTables wide_tables()
         for (int b = 0; b < 8; ++b)
             w.mac[8 * c + b] = J16::mac_base(mat_row((uint8_t)c, b));
     for (int t = 0; t < 6; ++t)
-        for (int r = 0; r < 14; ++r)
-            w.pre[14 * t + r] = (uint64_t)J16::pre_u32(t, 2 * r + 1) << 32 | J16::pre_u32(t, 2 * r);
+        for (int r = 0; r < WideTables::PW; ++r)
+            w.pre[WideTables::PW * t + r] = (uint64_t)J16::pre_u32(t, 2 * r + 1) << 32 | J16::pre_u32(t, 2 * r);
     return w;
 }
 

@@ -355,7 +355,10 @@ __global__ __launch_bounds__(64 * NV * TPW) __attribute__((amdgpu_num_vgpr(40)))
     // (workgroups that start later begin where the others are).
     // Rounded to the nearest period, so a workgroup starts with the chunk the
     // others are about to be in (same box x3, profiles/r05_rot/: C3 decode
-    // 22.53-22.58 ms at 600 ticks, 23.04-23.08 in order; 450-800 all gain).
+    // 22.53-22.58 ms at 600 ticks, 23.04-23.08 in order; 450-800 all gain;
+    // one process ABBA x10: the step -0.39 ms).  Re-picking the chunk before
+    // every barrier by the clock measured 0.8 ms slower than this
+    // (ab_knob_rot_mode2.json).
     int rot = 0;
     if (a.chunk_rot_ticks > 0) {
         __shared__ int s_rot;
@@ -395,8 +398,13 @@ __global__ __launch_bounds__(64 * NV * TPW) __attribute__((amdgpu_num_vgpr(40)))
         wait_vm(0);
         ph.mark(1);  // phase 1: this chunk's LDS-DMA
         {
-            auto transpose = [&](int t, uint4 u, uint4 v) {
-                const uint32_t m4 = vconst(0x0F0F0F0Fu), m2 = vconst(0x33333333u), m1 = vconst(0x55555555u);
+            // (Tried, round 5: the wave's three sources' LDS reads batched in
+            // hand-allocated asm, one exposed LDS latency per chunk instead of
+            // three -- the step unchanged in a same-process ABBA x10,
+            // profiles/r05_energy/ab_knob_asm_transposes.json; not kept.)
+            const uint32_t m4 = vconst(0x0F0F0F0Fu), m2 = vconst(0x33333333u), m1 = vconst(0x55555555u);
+            for (int t = wave; t < nt && RSGPU_DIAG_VAR != 5; t += NV) {
+                uint4 u = buf[(t * 2 + 0) * 64 + lane], v = buf[(t * 2 + 1) * 64 + lane];
                 uint32_t Wd[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
                 tr8(Wd, m4, m2, m1);
                 if constexpr (RSGPU_DIAG_VAR == 2) {  // zero planes, the transpose kept
@@ -408,36 +416,6 @@ __global__ __launch_bounds__(64 * NV * TPW) __attribute__((amdgpu_num_vgpr(40)))
                 }
                 buf[(t * 2 + 0) * 64 + lane] = make_uint4(Wd[0], Wd[1], Wd[2], Wd[3]);
                 buf[(t * 2 + 1) * 64 + lane] = make_uint4(Wd[4], Wd[5], Wd[6], Wd[7]);
-            };
-#ifndef RSGPU_JW_TR_BATCH
-#define RSGPU_JW_TR_BATCH 1
-#endif
-            if constexpr (RSGPU_JW_TR_BATCH && RSGPU_DIAG_VAR != 5 && RSGPU_DIAG_VAR != 2 && PW <= 3) {
-                // the wave's share (t = wave + NV i) in hand-allocated
-                // registers (gen_tc_handlers.py jw_transposes): the first two
-                // sources read together, the third while the second is
-                // transposed, so the chunk exposes one LDS latency instead of
-                // one per source (the compiler's 40 VGPRs spill doing this)
-                const uint32_t ta = lds0 + (uint32_t)(par * kBuf) + (uint32_t)wave * 2048 + lane * 16;
-                const int n = (wave < nt) + (wave + NV < nt) + (PW > 2 && wave + 2 * NV < nt);
-#define RSGPU_JW_TR(N, V) asm volatile(RSGPU_JW_TR##N##_NV##V ::"v"(ta) : RSGPU_JW_TR_CLOBBERS, "memory")
-                if constexpr (NV == 2) {
-                    if (n == 3)
-                        RSGPU_JW_TR(3, 2);
-                    else if (n == 2)
-                        RSGPU_JW_TR(2, 2);
-                    else if (n == 1)
-                        RSGPU_JW_TR(1, 2);
-                } else {
-                    if (n == 2)
-                        RSGPU_JW_TR(2, 4);
-                    else if (n == 1)
-                        RSGPU_JW_TR(1, 4);
-                }
-#undef RSGPU_JW_TR
-            } else {
-                for (int t = wave; t < nt && RSGPU_DIAG_VAR != 5; t += NV)
-                    transpose(t, buf[(t * 2 + 0) * 64 + lane], buf[(t * 2 + 1) * 64 + lane]);
             }
         }
         ph.mark(2);  // phase 2: transposes
@@ -591,7 +569,7 @@ __global__ __launch_bounds__(256) void k_jitw_emit(int k, int e, int row_base, i
                                                    uint8_t* code)
 {
     constexpr int R = W::R, CS = W::CS, PW = W::PRE / 8;
-    static_assert(PW == 14 && CS <= 6, "preamble table: 14 words per source, chunk positions < 6");
+    static_assert(PW == jit::WideTables::PW && CS <= 6, "preamble table: PW words per source, chunk positions < 6");
     __shared__ uint8_t cw[R * 256];
     const int b = blockIdx.y, w = blockIdx.x;
     if (status[b] != 0)

@@ -989,3 +989,29 @@ def test_wide_rows_decode_in_at_most_two_launches(ctx, k, e, L):
     apply = [n for n in names if n.startswith("k_rs_jit")]
     assert 1 <= len(apply) <= 2, names
     assert all(n == ("k_rs_jitw_passes(decode)" if e > 64 else "k_rs_jit16x4(decode)") for n in apply), names
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("period", [600, 1, 37, 0])
+@pytest.mark.parametrize("k,e,L,B", [(64, 32, 1000000, 2), (64, 32, 32000, 9), (100, 20, 6144, 3),
+                                     (64, 40, 65536, 3), (150, 100, 16384, 2), (18, 17, 4096, 3)])
+def test_jitw_chunk_rotation(ctx, period, k, e, L, B):
+    """k_rs_jitw's chunk order rotated by the workgroup's start time, for
+    periods that put neighbouring workgroups in different phases (1 tick) and
+    for none (0):
+    every chunk applied exactly once, so the same recovered bytes with the
+    erased rows poisoned -- two- and four-wave layouts, passes above 64 rows,
+    and a three-chunk block whose last chunk is partial (k 18, CS 5)."""
+    import ctypes
+    f_rot = rsgpu.testhooks().rsgpu_internal_set_jitw_rot
+    f_rot.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    ctx.set_decode_kernel("generated")
+    assert f_rot(ctx._h, period) == 0
+    try:
+        enc = rsgpu.GpuEncoder(k, L, e, blocks=B, seed=79, ctx=ctx)
+        enc.encode_all()
+        dec = rsgpu.GpuDecoder(k, L, e, blocks=B, seed=79, ctx=ctx)
+        assert decode_poisoned(ctx, enc, dec)
+    finally:
+        f_rot(ctx._h, -1)
+        ctx.set_decode_kernel("auto")
