@@ -312,7 +312,11 @@ __global__ __launch_bounds__(64 * NV * TPW) __attribute__((amdgpu_num_vgpr(40)))
     const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint4*)&lds[0][tw][0];
     constexpr uint32_t kBuf = TPW * CS * 2 * 64 * 16;  // bytes between the two chunk buffers
     const long long off = (RSGPU_DIAG_VAR == 1 ? (tile & 7) : tile) * 2048 + lane * 32;
-    const uint32_t loff = off + 32 <= a.len ? (uint32_t)off : 0u;  // tiles past the row re-read its head
+    // lanes past the row end re-read its head (results never stored; at C4
+    // 24 of 64 lanes of every row's last tile).  Loading nothing there cut
+    // the C4 decode's HBM bytes but not its time (3.26-3.28 vs 3.26-3.27 ms
+    // per slice, same box x3, round 5): the head is in L2.
+    const uint32_t loff = off + 32 <= a.len ? (uint32_t)off : 0u;
     if (wv == 0)
         asm volatile("s_icache_inv\n s_nop 15\n s_nop 15" ::: "memory");
     // the row pointers through the constant address space: scalar loads the

@@ -19,6 +19,18 @@ Everything is counted in wave64 VALU instructions per C3 column tile (2 KB x
 constant scaling (single-value outputs are renames), 36 per bit transpose.
 Every split is checked on random bytes against V itself first.
 
+What the counts do not show, and why the encode is not built this way
+(DESIGN §4): every Karatsuba form shares a product (X = B (x1 + x2)) between
+the top and the bottom output rows, which live in different waves.  A wave
+owns ONE set of 8-row accumulators and its sources arrive as a stream, so
+its share of X can reach the other wave only as a pure snapshot, which
+exists only if the wave finishes X before it starts its own Q rows -- and
+Q's sources (x1) are then streamed past it again (+25 % source traffic), or
+it holds X and Q in two accumulator sets (+64 VGPRs: 3 waves per SIMD, and
+the compiled 16-row encode already spills 416 VGPRs at that budget).  With
+the measured prices (profiles/r05_energy/: 1 KB of LDS per tile ~ 2.75
+VALU) neither leaves the >= 8 % the verdict asked for.
+
 usage: python3 tools/karatsuba_price.py [--out FILE.json]
 """
 from __future__ import annotations

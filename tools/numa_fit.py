@@ -65,7 +65,42 @@ def mode1(path):
         print(f"  bit {8 + i:2d}: {flips[i] / n:.3f}")
 
 
+def mode2(path):
+    """16 lines per 4 KB page from each XCC: the page is near XCC 0 when its
+    mean latency from XCC 0 is the lower.  Fits the side as an XOR of page
+    address bits (12..33), exhaustively over subsets of up to 3 bits."""
+    import itertools
+    off, l0, l1 = load(path)
+    pg = off >> 12
+    order = np.argsort(pg, kind="stable")
+    pg, l0, l1 = pg[order], l0[order], l1[order]
+    pages, idx = np.unique(pg, return_index=True)
+    m0 = np.add.reduceat(l0, idx) / np.diff(np.append(idx, len(pg)))
+    m1 = np.add.reduceat(l1, idx) / np.diff(np.append(idx, len(pg)))
+    near0 = (m0 < m1).astype(np.int64)
+    margin = np.abs(m0 - m1)
+    print(f"{path}: {len(pages)} pages, near XCC0 {near0.mean():.3f}, margin median {np.median(margin):.0f} "
+          f"(p10 {np.percentile(margin, 10):.0f}) cycles")
+    bits = list(range(12, 34))
+    B = np.array([[(int(p) << 12 >> b) & 1 for b in bits] for p in pages], np.int64)
+    best = (0, None, 0)
+    for r in (1, 2, 3):
+        for sub in itertools.combinations(range(len(bits)), r):
+            x = np.bitwise_xor.reduce(B[:, list(sub)], axis=1)
+            for c in (0, 1):
+                acc = ((x ^ c) == near0).mean()
+                if acc > best[0]:
+                    best = (acc, tuple(bits[i] for i in sub), c)
+    print(f"  best XOR of up to 3 page bits: {best[1]} ^ {best[2]} explains {best[0]:.4f}")
+    seq = pages < 4096
+    runs = np.diff(np.flatnonzero(np.diff(near0[seq]) != 0))
+    print("  first 16 MB, run lengths in pages:", np.unique(runs, return_counts=True))
+
+
 if __name__ == "__main__":
+    if len(sys.argv) > 1 and sys.argv[1] == "--mode2":
+        mode2(sys.argv[2])
+        sys.exit(0)
     mode0(sys.argv[1])
     if len(sys.argv) > 2:
         mode1(sys.argv[2])

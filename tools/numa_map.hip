@@ -7,7 +7,8 @@
 // tools/numa_fit.py fits the group as a function of the address bits.
 //   hipcc --offload-arch=gfx950 -O3 -o tools/numa_map tools/numa_map.hip
 //   tools/numa_map MODE > out.txt   (MODE 0: every 256 B of 32 MB; 1: bits
-//   8..33 one at a time over 256 random bases)
+//   8..33 one at a time over 256 random bases; 2: 16 lines per 4 KB page of
+//   the first 16 MB and of 2048 random pages)
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -59,6 +60,18 @@ int main(int argc, char** argv)
     if (mode == 0) {
         for (unsigned long long o = 0; o < (32ull << 20); o += 256)
             offs.push_back(o);
+    } else if (mode == 2) {
+        // 16 fresh 256-byte lines of each 4 KB page (XCC 1 takes the +128
+        // line of each): the first 4096 pages (16 MB), then 2048 random pages
+        std::mt19937_64 rng(11);
+        std::vector<unsigned long long> pages;
+        for (unsigned long long p = 0; p < 4096; ++p)
+            pages.push_back(p << 12);
+        for (int i = 0; i < 2048; ++i)
+            pages.push_back((rng() % ((bytes >> 1) >> 12)) << 12);
+        for (unsigned long long pg : pages)
+            for (int l = 0; l < 16; ++l)
+                offs.push_back(pg + 256ull * l);
     } else {
         std::mt19937_64 rng(7);
         for (int b = 0; b < 256; ++b) {
