@@ -39,6 +39,7 @@ ENC, DEC = "k_rs_bs(encode)", "k_rs_jit16(decode)"
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--blocks", type=int, default=1024)
+    ap.add_argument("--symbol-size", type=int, default=1000000, help="L (32000: C4's rows)")
     ap.add_argument("--seconds", type=float, default=2.5, help="per phase (ignored with --launches)")
     ap.add_argument("--launches", type=int, default=0, help="fixed launches per phase")
     ap.add_argument("--order", default="enc:rand,enc:zero,dec:zero,dec:rand,enc:rand,enc:zero,dec:zero,dec:rand")
@@ -56,7 +57,7 @@ def main() -> int:
         lib.rsgpu_diag_clock_read.restype = C.c_int
         lib.rsgpu_diag_clock_clear.restype = C.c_int
         lib.rsgpu_diag_clock_slots.restype = C.c_int
-    k, e, L, B = 64, 32, 1000000, args.blocks
+    k, e, L, B = 64, 32, args.symbol_size, args.blocks
     ctx = rsgpu.Context(0)
     ctx.set_torch_stream()
     enc = rsgpu.GpuEncoder(k, L, e, blocks=B, seed=1, ctx=ctx)
@@ -159,7 +160,7 @@ def main() -> int:
         print(json.dumps(ph), flush=True)
 
     out = {"tool": "tools/bound_probe.py", "library": rsgpu.LIB_PATH, "diagnostic_build": diag,
-           "workload": f"C3 k={k} e={e} L={L} blocks={B}", "alg_bytes_per_launch": alg,
+           "workload": f"k={k} e={e} L={L} blocks={B}", "alg_bytes_per_launch": alg,
            "phases": phases, "dispatches": dispatches}
     if args.out:
         os.makedirs(os.path.dirname(os.path.abspath(args.out)), exist_ok=True)
