@@ -42,6 +42,7 @@ def main() -> int:
     ap.add_argument("--symbol-size", type=int, default=1000000)
     ap.add_argument("--erased", type=int, default=32)
     ap.add_argument("--blocks", type=int, default=1024)
+    ap.add_argument("--encode-kernel", default=None, help="fixed encode kernel for every configuration")
     ap.add_argument("--out", default=None)
     args = ap.parse_args()
 
@@ -54,6 +55,8 @@ def main() -> int:
     enc = rsgpu.GpuEncoder(k, L, e, blocks=B, seed=1, ctx=ctx)
     dec = rsgpu.GpuDecoder(k, L, e, blocks=B, seed=1, ctx=ctx)
     vals = args.values.split(",")
+    if args.encode_kernel:
+        ctx.set_encode_kernel(args.encode_kernel)
 
     def apply(v):
         if args.knob == "encode_kernel":
