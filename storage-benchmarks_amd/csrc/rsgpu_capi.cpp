@@ -380,6 +380,12 @@ int shared_program_launch(rsgpu_ctx* ctx, const uint8_t* coef, int k, int rows, 
             j.len = len;
             j.status = nullptr;
             j.tiles_per_wg = 2;
+            // every block on the same code: the start-time chunk rotation
+            // (k_rs_jitw) lines up the workgroups of a CU pair on one chunk
+            // (same-process ABBA x6, profiles/r05_rot/shared/: C5 encode 12.96
+            // -> 12.37 ms, step -2.7 %; (48, 24) step -0.7 %; C3's generated
+            // encode 22.65 -> 21.73 ms, still 1.7 % behind k_rs_bs)
+            j.chunk_rot_ticks = ctx->jitw_rot >= 0 ? ctx->jitw_rot : jitw_rot_ticks(j.rows);
             KTimer kt(ctx, name, (size_t)blocks);
             RS_HIP(ctx, launch_rs_jitw(j, blocks, ctx->stream));
         }
@@ -1226,8 +1232,10 @@ int jitw_launch(rsgpu_ctx* ctx, int k, int e, size_t len, size_t blocks, const u
         }
         // chunk order rotated by each workgroup's start time, so the
         // workgroups sharing a CU pair's instruction cache walk their block's
-        // code in step (k_rs_jitw)
-        j.chunk_rot_ticks = ctx->jitw_rot >= 0 ? ctx->jitw_rot : jitw_rot_ticks(rows);
+        // code in step (k_rs_jitw).  Not for short rows: a block's few
+        // workgroups run its code once each, and the rotation measured +0.5 %
+        // on the C4 step (same-process ABBA x6, profiles/r05_rot/shared/)
+        j.chunk_rot_ticks = ctx->jitw_rot >= 0 ? ctx->jitw_rot : j.code_prefetch ? 0 : jitw_rot_ticks(rows);
         const int r = jitw_rows(rows);
         KTimer kt(ctx,
                   e > 64  ? "k_rs_jitw_passes(decode)"
