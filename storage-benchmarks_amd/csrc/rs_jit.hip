@@ -365,7 +365,16 @@ __global__ __launch_bounds__(64 * NV * TPW) __attribute__((amdgpu_num_vgpr(40)))
     // (ab_knob_rot_mode2.json).
     int rot = 0;
     if (a.chunk_rot_ticks > 0) {
-        __shared__ int s_rot;
+        // broadcast through the first word of chunk buffer 1, which no
+        // LDS-DMA writes before the first chunk barrier: a separate
+        // __shared__ int made the 10-row two-tile kernel 40964 bytes, four
+        // bytes too many for four workgroups per CU
+#ifdef RSGPU_AB_SROT_SEPARATE  // the round-5 A/B's baseline only
+        __shared__ int s_rot_sep;
+        volatile int& s_rot = s_rot_sep;
+#else
+        volatile int& s_rot = *(volatile int*)&lds[1][0][0];
+#endif
         if (threadIdx.x == 0) {
             unsigned long long t;
             asm volatile("s_memrealtime %0\n s_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");

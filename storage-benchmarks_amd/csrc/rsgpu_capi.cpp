@@ -379,7 +379,7 @@ int shared_program_launch(rsgpu_ctx* ctx, const uint8_t* coef, int k, int rows, 
             j.dst_stride = rows;
             j.len = len;
             j.status = nullptr;
-            j.tiles_per_wg = 2;
+            j.tiles_per_wg = ctx->jitw_tpw ? ctx->jitw_tpw : 2;
             // every block on the same code: the start-time chunk rotation
             // (k_rs_jitw) lines up the workgroups of a CU pair on one chunk
             // (same-process ABBA x6, profiles/r05_rot/shared/: C5 encode 12.96
