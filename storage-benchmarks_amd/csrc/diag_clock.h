@@ -30,6 +30,11 @@
 //   7 code0   k_rs_jitw runs block 0's code in every block (L2-resident code)
 //   8 chunk0  k_rs_jitw runs each wave's chunk-0 code for every full chunk
 //             (instruction-cache-resident code)
+//   9, 10     marginal LDS / VALU prices of the generated decode (rs_jit.h)
+//   11 lfix   every multiply-accumulate of the generated code reads the same
+//             low-nibble composite (one operand's data constant between
+//             consecutive instructions; same instruction count)
+//   12 lhfix  both composite operands fixed the same way
 #if defined(RSGPU_DIAG_CLOCK) && defined(RSGPU_DIAG_VARIANT)
 #define RSGPU_DIAG_VAR RSGPU_DIAG_VARIANT
 #else

@@ -260,6 +260,15 @@ struct Wide {
     RJ_HD static constexpr uint64_t mac_base(uint8_t m)
     {
         const int lo = m & 15, hi = m >> 4;
+        // diagnostic variants 11 / 12 (diag_clock.h): operand data held
+        // constant between consecutive multiply-accumulates (timing only)
+        if constexpr (RSGPU_JIT_DIAG_VAR == 11 || RSGPU_JIT_DIAG_VAR == 12) {
+            const int l = 1, h = RSGPU_JIT_DIAG_VAR == 12 ? 1 : hi;
+            return lo && hi ? enc_bitop3_96(0, 0, treg(0, l), treg(1, h))
+                   : lo     ? enc_xor_e64(0, 0, treg(0, l))
+                   : hi     ? enc_xor_e64(0, 0, treg(1, h))
+                            : NOP2;
+        }
         return lo && hi ? enc_bitop3_96(0, 0, treg(0, lo), treg(1, hi))
                : lo     ? enc_xor_e64(0, 0, treg(0, lo))
                : hi     ? enc_xor_e64(0, 0, treg(1, hi))
