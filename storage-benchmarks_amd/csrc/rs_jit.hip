@@ -668,10 +668,14 @@ int jitw_rows(int e)
 
 int jitw_rot_ticks(int rows)
 {
-    // one chunk's work per wave, CS (8 R + 24) VALU, scaled from C3's
-    // measured optimum (R 16, CS 6: 600 ticks)
-    const int r = jitw_rows(rows), cs = jitw_cs(rows);
-    return r ? 600 * cs * (8 * r + 24) / (6 * (8 * 16 + 24)) : 0;
+    // one chunk's work per wave, CS (8 R + 24) VALU, times the waves sharing
+    // a SIMD (4 for the 10-row kernels, 3 otherwise), scaled from C3's
+    // measured optimum (R 16, CS 6, 3 waves: 600 ticks).  C5 (R 10): 456;
+    // 500 measured 0.6 % faster than 342 and 200 1.1 % slower
+    // (profiles/r05_rot/c5_period.json); 456 against 342 same process ABBA
+    // x6: -0.14 ms per C5 step (c5_period_456_vs_342.json)
+    const int r = jitw_rows(rows), cs = jitw_cs(rows), waves = r == 10 ? 4 : 3;
+    return r ? 600 * cs * (8 * r + 24) * waves / (6 * (8 * 16 + 24) * 3) : 0;
 }
 
 int jitw_cs(int e) { return jitw_rows(e) == 16 ? jit::J16::CS : jitw_rows(e) == 12 ? jit::J12::CS : jit::J10::CS; }
