@@ -369,12 +369,7 @@ __global__ __launch_bounds__(64 * NV * TPW) __attribute__((amdgpu_num_vgpr(40)))
         // LDS-DMA writes before the first chunk barrier: a separate
         // __shared__ int made the 10-row two-tile kernel 40964 bytes, four
         // bytes too many for four workgroups per CU
-#ifdef RSGPU_AB_SROT_SEPARATE  // the round-5 A/B's baseline only
-        __shared__ int s_rot_sep;
-        volatile int& s_rot = s_rot_sep;
-#else
         volatile int& s_rot = *(volatile int*)&lds[1][0][0];
-#endif
         if (threadIdx.x == 0) {
             unsigned long long t;
             asm volatile("s_memrealtime %0\n s_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
@@ -689,10 +684,6 @@ size_t jitw_chunk_stride(int e)
 // the layout covers e: 16 < e <= 64 in one launch, 64 < e <= 125 in passes
 bool jitw_layout(int e)
 {
-#ifdef RSGPU_AB_JIT8  // A/B build only: the 4 x 8-row layout for e <= 32
-    if (e <= 32)
-        return false;
-#endif
     return e > 16 && (e <= 64 || (e <= 128 && jitw_rows(jit::wide_pass_rows(e, 0)) &&
                                                         jitw_rows(jit::wide_pass_rows(e, jit::wide_passes(e) - 1))));
 }
