@@ -23,7 +23,10 @@ each process is one rank; `python bench.py --gpus N` without a launcher
 spawns the N rank processes itself (the parent never touches the GPU).  Each
 rank owns its own shard of blocks (weak scaling, no collective on the data
 path); torch.distributed only carries the barrier and the
-max-over-ranks time.
+max-over-ranks time, over gloo by default (host TCP, initialised before the
+GPU is touched; RCCL only with --dist-backend nccl).  A rank that fails
+leaves its error in the process group's store, and rank 0 prints one JSON
+line naming every failed rank.
 
 Prints ONE JSON line on rank 0.
 """
@@ -90,10 +93,14 @@ def parse(argv=None):
                         "tools/pmc_summary.py): VALU-issue roofline of each kernel")
     p.add_argument("--valu-ceiling", default=os.path.join(ROOT, "profiles", "r03_valu_ceiling.json"),
                    help="measured VALU issue ceiling (tools/ubench_issue + tools/valu_ceiling.py)")
-    # testing the N-rank path on a one-GPU box: every rank on device 0, gloo
-    # for the barrier / max-time reduction (RCCL needs one GPU per rank)
+    # testing the N-rank path on a one-GPU box: every rank on device 0
     p.add_argument("--same-device", action="store_true", help=argparse.SUPPRESS)
-    p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"])
+    # the collectives (barrier, max time, shard info, verification) lie
+    # outside the timed data path: gloo over host TCP by default, so the
+    # 8-rank start-up never depends on a multi-rank RCCL init
+    p.add_argument("--dist-backend", default="gloo", choices=["gloo", "nccl"])
+    p.add_argument("--dist-timeout", type=float, default=900.0,
+                   help="seconds a collective waits for the other ranks")
     return p.parse_args(argv)
 
 
@@ -139,10 +146,11 @@ def free_port() -> int:
         return s.getsockname()[1]
 
 
-def spawn_ranks(n: int, argv) -> int:
+def spawn_ranks(n: int, argv, grace: float = 60.0) -> int:
     """`bench.py --gpus N` without a launcher: start N rank processes of this
     script (this parent has not touched the GPU), wait for all, return the
-    worst exit status.  A failing rank takes the others down."""
+    worst exit status.  After a rank fails the others get `grace` seconds to
+    notice (rank 0 then prints the line naming it) before they are stopped."""
     port = str(free_port())
     procs = []
     for r in range(n):
@@ -153,6 +161,7 @@ def spawn_ranks(n: int, argv) -> int:
                                       env=env))
     rc = 0
     alive = list(procs)
+    stop_at = None
     while alive:
         for p in list(alive):
             r = p.poll()
@@ -160,9 +169,12 @@ def spawn_ranks(n: int, argv) -> int:
                 continue
             alive.remove(p)
             rc = max(rc, abs(r))
-            if r != 0:
-                for q in alive:
-                    q.terminate()
+            if r != 0 and stop_at is None:
+                stop_at = time.time() + grace
+        if stop_at is not None and time.time() >= stop_at:
+            for q in alive:
+                q.terminate()
+            stop_at = float("inf")
         time.sleep(0.05)
     return rc
 
@@ -507,8 +519,8 @@ def c1_line(args) -> dict:
     head = legs[0]
     ok = all(lg["failures"] == 0 for lg in legs)
     return {
-        "metric": "encode+decode goodput GiB/s (device-resident) at symbols x symbol_size; "
-                  "%HBM roofline",
+        # not the GPU metric: the same accounting on the host CPU
+        "metric": "encode+decode goodput GiB/s on the host CPU (reference accounting)",
         "value": round(head["goodput_GiBps"], 4), "unit": "GiB/s", "n_gpus": 0,
         "steps": head["blocks_per_thread"], "warmup": 0,
         "ms_per_step": round((head["encode_us_per_block"] + head["decode_us_per_block"]) / 1e3, 4),
@@ -775,13 +787,105 @@ def run_streamed(args, rsgpu, ctx, dev, rank, world, k, e, L, total_blocks):
     return timed, wall, int(mism.sum().item()), nb_total, batch, recs, batch_ms
 
 
+METRIC = ("encode+decode goodput GiB/s (device-resident) at symbols x symbol_size; "
+          "%HBM roofline")
+FAIL_KEY = "bench_py/failed/{}"
+
+
+def init_dist(args, world, device_index):
+    """The process group of a multi-rank run.  Returns (store, device of the
+    reductions).  gloo (the default) is set up over host TCP before this
+    process makes any GPU call; nccl (RCCL, --dist-backend nccl) after the
+    rank's device is selected.  One rank: no process group, (None, cpu)."""
+    import datetime
+
+    import torch
+    import torch.distributed as dist
+    if world <= 1:
+        return None, torch.device("cpu")
+    if args.dist_backend == "nccl":
+        torch.cuda.set_device(device_index)
+    dist.init_process_group(args.dist_backend, init_method="env://",
+                            timeout=datetime.timedelta(seconds=args.dist_timeout))
+    store = dist.distributed_c10d._get_default_store()
+    red = torch.device("cuda", device_index) if args.dist_backend == "nccl" else torch.device("cpu")
+    return store, red
+
+
+def failure_record(rank, ex) -> dict:
+    """What a failed rank leaves for rank 0: its error and the innermost frames."""
+    import traceback
+    tb = "".join(traceback.format_exception(type(ex), ex, ex.__traceback__)[-3:])
+    return {"rank": rank, "error": f"{type(ex).__name__}: {ex}"[:1000], "where": tb[-1500:],
+            "t": time.time()}
+
+
+def collect_failures(store, world, own, wait_s):
+    """Rank 0: the records every failed rank left in the store, polled for up
+    to wait_s (a peer's failure usually reaches rank 0 as a closed connection
+    before its record is read), earliest first -- the first is the cause."""
+    found = {own["rank"]: own}
+    deadline = time.time() + wait_s
+    while True:
+        for r in range(world):
+            key = FAIL_KEY.format(r)
+            if r not in found:
+                try:
+                    if store.check([key]):
+                        found[r] = json.loads(store.get(key).decode())
+                except Exception:  # the store is rank 0's own: only a torn read
+                    pass
+        if len(found) == world or time.time() >= deadline:
+            break
+        time.sleep(0.2)
+    return sorted(found.values(), key=lambda f: f.get("t", 0.0))
+
+
+def failure_line(args, world, failed) -> dict:
+    """The one JSON line of a failed run: no value, every failed rank named."""
+    return {"metric": METRIC, "value": None, "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": None, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+            "config": {"workload": f"isa_throughput {args.config}", "dist_backend": args.dist_backend},
+            "verified": False, "roofline": None, "cpu_baseline": None,
+            "error": {"failed_ranks": [f["rank"] for f in failed], "first": failed[0],
+                      "all": failed}}
+
+
+def report_failure(args, rank, world, store, ex, wait_s=10.0):
+    """A rank's exception: its record goes to the process group's store; rank
+    0 gathers every rank's record and prints the run's one JSON line.
+    Returns (exit status, the line or None)."""
+    rec = failure_record(rank, ex)
+    print(f"bench.py rank {rank}: {rec['error']}\n{rec['where']}", file=sys.stderr, flush=True)
+    if store is not None:
+        try:
+            store.set(FAIL_KEY.format(rank), json.dumps(rec))
+        except Exception:  # rank 0 (the store's host) is gone: it reports nothing then
+            pass
+    if rank != 0:
+        return 1, None
+    failed = collect_failures(store, world, rec, wait_s) if store is not None and world > 1 else [rec]
+    line = failure_line(args, world, failed)
+    print(json.dumps(line), flush=True)
+    return 1, line
+
+
 def main(argv=None):
     argv = sys.argv[1:] if argv is None else argv
     args = parse(argv)
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        if args.config == "c1":
+            print("bench.py: --config c1 is one host-CPU line; run it without --gpus", file=sys.stderr)
+            return 2
         # no launcher: this process only spawns the ranks (never touches the GPU)
         return spawn_ranks(args.gpus, argv)
     if args.config == "c1":  # host only: neither torch's GPU side nor the engine
+        if args.symbols is not None or args.symbol_size is not None or args.loss_rate is not None \
+                or args.blocks is not None:
+            print("bench.py: --config c1 is the reference's fixed CPU case (16, 64000, 0.5); "
+                  "geometry flags are not taken", file=sys.stderr)
+            return 2
         print(json.dumps(c1_line(args)), flush=True)
         return 0
     rank, world, local = dist_env()
@@ -789,15 +893,31 @@ def main(argv=None):
         print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
         return 2
 
-    import torch
     import torch.distributed as dist
 
     device_index = 0 if args.same_device else local
-    torch.cuda.set_device(device_index)
+    store = None
+    try:
+        store, red_dev = init_dist(args, world, device_index)
+        rc = run_rank(args, rank, world, device_index, red_dev)
+    except Exception as ex:
+        rc, _ = report_failure(args, rank, world, store, ex)
+        # no destroy_process_group: the peers may be gone
+        return rc
     if world > 1:
-        dist.init_process_group(args.dist_backend, init_method="env://")
+        dist.destroy_process_group()
+    return rc
+
+
+def run_rank(args, rank, world, device_index, red_dev):
+    """One rank's run (the process group, if any, is up): build the batch,
+    warm up, time, verify; rank 0 prints the JSON line.  Returns the exit
+    status."""
+    import torch
+    import torch.distributed as dist
+
+    torch.cuda.set_device(device_index)
     dev = torch.device("cuda", device_index)
-    red_dev = dev if args.dist_backend == "nccl" else torch.device("cpu")
 
     import rsgpu
 
@@ -937,8 +1057,7 @@ def main(argv=None):
     step_frac = (2 * op_bytes) / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBPS
 
     line = {
-        "metric": "encode+decode goodput GiB/s (device-resident) at symbols x symbol_size; "
-                  "%HBM roofline",
+        "metric": METRIC,
         "value": round(value, 2), "unit": "GiB/s", "n_gpus": world, "steps": steps,
         "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
@@ -990,10 +1109,9 @@ def main(argv=None):
                 line["cpu_baseline_reference"] = cpu_baseline(k, e, L, threads, kernel=0)
         except Exception as ex:  # reported, never fatal for the GPU number
             line["cpu_baseline"] = {"error": str(ex), **host}
+    line["config"]["dist_backend"] = args.dist_backend if world > 1 else None
     if rank == 0:
         print(json.dumps(line), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
     return 0 if ok else 1
 
 

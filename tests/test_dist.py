@@ -87,3 +87,90 @@ def test_split_covers_every_block_once(total, world):
     assert owned == list(range(total))
     sizes = [n for _, n in shares]
     assert max(sizes) - min(sizes) <= 1
+
+
+def _default_backend_worker(rank, world, port, outdir):
+    """bench.init_dist with bench.py's default arguments: a gloo group, no
+    GPU call before it (RCCL never initialised)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    args = bench.parse(["--gpus", str(world)])
+    store, red = bench.init_dist(args, world, rank)
+    info = {"backend": dist.get_backend(), "red": str(red), "cuda_init": torch.cuda.is_initialized(),
+            "nccl_avail_used": dist.is_nccl_available() and dist.get_backend() == "nccl",
+            "store": store is not None}
+    t = bench.reduce_max_time(0.5 + rank, world, red)
+    info["t"] = t
+    dist.destroy_process_group()
+    np.save(os.path.join(outdir, f"d{rank}.npy"), np.array([repr(info)]))
+
+
+def test_default_backend_is_gloo_and_touches_no_gpu(tmp_path):
+    """the barrier / max-time / verification reductions
+    run over gloo unless --dist-backend nccl is given, set up before any GPU
+    call, so the driver's 8-rank start-up never depends on a multi-rank RCCL
+    init."""
+    assert bench.parse([]).dist_backend == "gloo"
+    world = 2
+    mp.spawn(_default_backend_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    for r in range(world):
+        info = eval(str(np.load(tmp_path / f"d{r}.npy")[0]))
+        assert info["backend"] == "gloo" and info["red"] == "cpu" and info["store"]
+        assert not info["cuda_init"] and not info["nccl_avail_used"]
+        assert info["t"] == 1.5
+
+
+def _failing_rank_worker(rank, world, port, outdir):
+    """Rank 1 fails on its own; rank 0, waiting in a barrier, sees the
+    closed connection and reports -- naming rank 1 first."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    args = bench.parse(["--gpus", str(world)])
+    store, red = bench.init_dist(args, world, rank)
+    try:
+        if rank == 1:
+            raise RuntimeError("simulated HIP error on rank 1")
+        dist.barrier()
+        raise AssertionError("barrier passed with rank 1 gone")
+    except Exception as ex:
+        rc, line = bench.report_failure(args, rank, world, store, ex, wait_s=20.0)
+    if rank == 0:
+        with open(os.path.join(outdir, "line.json"), "w") as f:
+            f.write(__import__("json").dumps(line))
+    os._exit(rc)  # no destroy: the peer is gone
+
+
+def test_failed_rank_is_named_by_rank0(tmp_path):
+    import json
+    world = 2
+    ctx = mp.start_processes(_failing_rank_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world,
+                             join=False, start_method="spawn")
+    for p in ctx.processes:
+        p.join(120)
+    assert all(p.exitcode == 1 for p in ctx.processes), [p.exitcode for p in ctx.processes]
+    line = json.loads((tmp_path / "line.json").read_text())
+    assert line["value"] is None and line["verified"] is False and line["n_gpus"] == 2
+    assert line["error"]["first"]["rank"] == 1
+    assert "simulated HIP error on rank 1" in line["error"]["first"]["error"]
+    assert sorted(line["error"]["failed_ranks"]) == [0, 1]
+
+
+def test_bench_ranks_on_cpu_report_their_failure():
+    """`bench.py --gpus 2` end to end on this GPU-less host: the spawned ranks
+    set up gloo, then fail at their first GPU call; rank 0 prints ONE JSON
+    line naming both ranks (the line the driver keeps instead of nothing)."""
+    import json
+    import subprocess
+    import sys
+    env = dict(os.environ, HIP_VISIBLE_DEVICES="")
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, os.path.join(os.path.dirname(bench.__file__), "bench.py"),
+                        "--gpus", "2", "--steps", "1", "--warmup", "0", "--no-cpu-baseline"],
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode != 0
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout + r.stderr[-2000:]
+    line = json.loads(lines[0])
+    assert line["value"] is None and sorted(line["error"]["failed_ranks"]) == [0, 1]
+    assert line["config"]["dist_backend"] == "gloo"
+    assert "nccl" not in r.stderr.lower()

@@ -375,11 +375,13 @@ def run_bench(args, timeout=600):
 
 def test_bench_spawns_its_own_ranks():
     """`bench.py --gpus 2` with no launcher starts two rank processes (here
-    both on device 0, gloo for the barrier): disjoint contiguous shards,
-    erasure lists drawn from the global block index, n_gpus 2, verified."""
-    line = run_bench(["--gpus", "2", "--same-device", "--dist-backend", "gloo", "--config", "c3",
+    both on device 0) on the DEFAULT backend (gloo):
+    disjoint contiguous shards, erasure lists drawn from the global block
+    index, n_gpus 2, verified."""
+    line = run_bench(["--gpus", "2", "--same-device", "--config", "c3",
                       "--blocks", "4", "--steps", "2", "--warmup", "1", "--no-cpu-baseline"])
     assert line["n_gpus"] == 2 and line["verified"]
+    assert line["config"]["dist_backend"] == "gloo"
     ranks = sorted(line["ranks"], key=lambda r: r["rank"])
     assert [(r["block0"], r["blocks"]) for r in ranks] == [(0, 4), (4, 4)]
     for r in ranks:
@@ -390,14 +392,15 @@ def test_bench_spawns_its_own_ranks():
 def test_bench_under_torch_distributed_run():
     """The driver's scaling launch: `python -m torch.distributed.run
     --nproc-per-node 2 ... bench.py --gpus 2` (ranks from WORLD_SIZE/RANK in
-    the environment, no self-spawn), here both ranks on device 0 over gloo."""
+    the environment, no self-spawn), here both ranks on device 0 on the
+    default backend (gloo)."""
     import socket
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(port),
-           os.path.join(ROOT, "bench.py"), "--gpus", "2", "--same-device", "--dist-backend", "gloo",
+           os.path.join(ROOT, "bench.py"), "--gpus", "2", "--same-device",
            "--config", "c3", "--blocks", "4", "--steps", "2", "--warmup", "1", "--no-cpu-baseline"]
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env)
@@ -413,7 +416,7 @@ def test_bench_under_torch_distributed_run():
 def test_rccl_path_single_rank():
     """The collectives bench.py runs between ranks (barrier, all_reduce MAX of
     the timed region, all_gather_object of the shards, all_reduce of the
-    mismatch count) on the default `nccl` backend, i.e. RCCL, in a world of
+    mismatch count) on the optional `nccl` backend (--dist-backend nccl), i.e. RCCL, in a world of
     one rank on this GPU: the only RCCL run a one-GPU box allows (two ranks
     cannot share a device under RCCL).  A subprocess owns the process group."""
     import socket

@@ -125,3 +125,13 @@ def test_bench_c1_cpu_line():
     assert line["value"] == round(line["legs"][0]["goodput_GiBps"], 4) > 0
     assert line["cpu_baseline"]["kind"] == "reference" and line["cpu_baseline"]["cores"] == 1
     assert "rsgpu" not in r.stderr
+
+
+def test_bench_c1_rejects_geometry_and_gpus():
+    """--config c1 is the reference's fixed CPU case: custom geometry and
+    --gpus > 1 (N ranks timing the CPU on shared cores) are refused."""
+    import sys
+    for extra in (["--symbols", "32"], ["--gpus", "2"], ["--blocks", "3"]):
+        r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--config", "c1"] + extra,
+                           capture_output=True, text=True, timeout=120)
+        assert r.returncode == 2 and "c1" in r.stderr, (extra, r.stderr)
