@@ -306,6 +306,98 @@ def karatsuba_rec(levels: int):
             "transposes": (K + E) * TR8, "total": tot + adds + d1 + d2 + (K + E) * TR8}
 
 
+# ---- Karatsuba inside ONE wave's rows ---------------------
+# A wave owns R output rows r in [R w, R w + R) of a Horner chunk of C = 16
+# sources; its R x R blocks of the Hankel form (g(n) = h(R w + j0 + n)) split
+# into top / bottom row halves and a source pair (x1, x2) of m = R / 2 each:
+#   P = B (x1 + x2),  top += P + (A + B) x1,  bottom += P + (C + B) x2,
+# all three Hankel again, so the split recurses.  P reaches both halves with
+# no second accumulator set: top ^= bottom; bottom += P; top ^= bottom (two
+# vector additions, 16 m VALU).  Real sources keep the D2 scaling folded into
+# their coefficients; a virtual source x1 s1 + x2 s2 is formed explicitly
+# (16 VALU from the two sources' tables, 8 for two virtual ones); D1 once per
+# row and tile at the end (the Horner twiddle 2^(C r) is unchanged).
+def inwave_cost(g, m, srcs, lv):
+    """VALU of y[r] = sum_q g[r + q] src_q, r < m, inside one wave; srcs are
+    the folded scales of real sources (None: a virtual source)."""
+    if lv == 0 or m < 4:
+        tot = 0
+        for q, s in enumerate(srcs):
+            c, mm = source_cost([MUL[g[r + q]][s] if s is not None else g[r + q] for r in range(m)])
+            tot += c + mm
+        return tot, {"leaf": tot}
+    hm = m // 2
+    x1, x2 = srcs[:hm], srcs[hm:]
+    virt = sum(VADD if a is None and b is None else 2 * VADD for a, b in zip(x1, x2))
+    gB = [g[n + hm] for n in range(2 * hm - 1)]
+    gQ1 = [g[n] ^ g[n + hm] for n in range(2 * hm - 1)]
+    gQ2 = [g[n + 2 * hm] ^ g[n + hm] for n in range(2 * hm - 1)]
+    cP, _ = inwave_cost(gB, hm, [None] * hm, lv - 1)
+    cQ1, _ = inwave_cost(gQ1, hm, x1, lv - 1)
+    cQ2, _ = inwave_cost(gQ2, hm, x2, lv - 1)
+    tb = 2 * VADD * hm
+    return cP + cQ1 + cQ2 + virt + tb, {"P": cP, "Q1": cQ1, "Q2": cQ2, "virtual_sources": virt,
+                                        "P_into_both_halves": tb}
+
+
+def inwave_eval(g, m, xs, lv):
+    """The same recursion on byte vectors (xs already scaled by D2)."""
+    if lv == 0 or m < 4:
+        return [matvec([[g[r + q] for q in range(m)]], xs)[0] for r in range(m)]
+    hm = m // 2
+    x1, x2 = xs[:hm], xs[hm:]
+    v = [vadd(a, b) for a, b in zip(x1, x2)]
+    P = inwave_eval([g[n + hm] for n in range(2 * hm - 1)], hm, v, lv - 1)
+    Q1 = inwave_eval([g[n] ^ g[n + hm] for n in range(2 * hm - 1)], hm, x1, lv - 1)
+    Q2 = inwave_eval([g[n + 2 * hm] ^ g[n + hm] for n in range(2 * hm - 1)], hm, x2, lv - 1)
+    return [vadd(p, q) for p, q in zip(P, Q1)] + [vadd(p, q) for p, q in zip(P, Q2)]
+
+
+def inwave_tile(R: int, lv: int, C: int = 16, check=True):
+    """One C3 column tile with E / R waves of R rows, Horner chunks of C."""
+    tot, parts = 0, {}
+    rng = random.Random(R * 10 + lv)
+    for w in range(E // R):
+        for j0 in range(0, C, R):
+            g = [h(R * w + j0 + n) for n in range(2 * R - 1)]
+            if check:
+                d = [[rng.randrange(256) for _ in range(4)] for _ in range(R)]
+                y = inwave_eval(g, R, [vmul(gpow(-c2(j0 + q)), d[q]) for q in range(R)], lv)
+                for r in range(R):
+                    row = R * w + r
+                    want = matvec([[gpow(row * (j0 + q)) for q in range(R)]], d)[0]
+                    assert vmul(gpow(c2(row)), want) == y[r], ("in-wave split disagrees with V", R, lv, row)
+            c, p = inwave_cost(g, R, [gpow(-c2(j0 + q)) for q in range(R)], lv)
+            tot += c
+            for key, v in p.items():
+                parts[key] = parts.get(key, 0) + v
+    tot *= K // C
+    parts = {key: v * (K // C) for key, v in parts.items()}
+    tw = sum(scale_cost(gpow(C * r)) for r in range(E)) * (K // C - 1)
+    d1 = sum(scale_cost(gpow(-c2(r))) for r in range(E))
+    tr = (K + E) * TR8
+    return {"rows_per_wave": R, "levels": lv, "products_and_adds": tot, "parts": parts, "twiddles": tw,
+            "d1": d1, "transposes": tr, "total": tot + tw + d1 + tr,
+            "vgprs": "accumulators 8 R + planes 8 + composites <= 22 + one virtual source's 8 planes"}
+
+
+def direct_rows(R: int, C: int = 16):
+    """The plain compiled encode with R rows per wave (no split): R = 8 is
+    k_rs_bs<64, 32, 16, 4> without T0Pair, R = 16 round 4's two-wave layout."""
+    comp = mac = 0
+    for g in range(E // R):
+        for T in range(C):
+            c, m = source_cost([gpow(r * T) for r in range(g * R, (g + 1) * R)])
+            comp += c
+            mac += m
+    comp *= K // C
+    mac *= K // C
+    tw = sum(scale_cost(gpow(C * r)) for r in range(E)) * (K // C - 1)
+    tr = (K + E) * TR8
+    return {"rows_per_wave": R, "composites": comp, "macs": mac, "twiddles": tw, "transposes": tr,
+            "total": comp + mac + tw + tr}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=None)
@@ -319,6 +411,11 @@ def main():
            "measured_k_rs_bs_valu_per_tile": round(1.201e10 / (489 * 1024), 1),
            "current_model": cur, "karatsuba_1level_layout": k1, "karatsuba_1level_balanced": bal,
            "karatsuba_1level_floor": rec1}
+    res["in_wave"] = {"direct_R8": direct_rows(8), "direct_R16": direct_rows(16)}
+    for R, lv in ((16, 1), (16, 2), (8, 1)):
+        res["in_wave"][f"karatsuba_R{R}_levels{lv}"] = inwave_tile(R, lv)
+    res["in_wave_cut_vs_model"] = {key: round(1 - v["total"] / cur["total"], 4)
+                                   for key, v in res["in_wave"].items()}
     res["cut_vs_model"] = {"karatsuba_1level_layout": round(1 - k1["total"] / cur["total"], 4),
                            "karatsuba_1level_balanced": round(1 - bal["total"] / cur["total"], 4),
                            "karatsuba_1level_floor": round(1 - rec1["total"] / cur["total"], 4)}
