@@ -13,33 +13,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-// Timing-only energy variants of the diagnostic build (round 5,
-// tools/energy_run.sh; make diag DIAG_VARIANT=n): the same instruction
-// stream with one component's data made quiet, or one phase removed.  Their
-// outputs are WRONG by construction; the product build always has 0.
-//   1 hbmq    sources read from, rows written to, a window of two blocks x
-//             16 KB per row that stays in the XCD's L2 (HBM I/O quiet)
-//   2 zplane  the transposes write zero planes (LDS plane writes and reads,
-//             the VALU of the multiply-accumulates and the row stores quiet)
-//   3 valuq   the planes are read from LDS as usual but land in dead
-//             registers, the VALU works on zero planes (VALU quiet)
-//   4 nowait  the generated decode's per-source LDS wait removed
-//   5 notr    the source transposes skipped (raw bytes used as planes)
-//   6 phases  the product stream plus s_memtime stamps between the phases of
-//             k_rs_jitw (per-wave cycle sums of one workgroup in kEvery)
-//   7 code0   k_rs_jitw runs block 0's code in every block (L2-resident code)
-//   8 chunk0  k_rs_jitw runs each wave's chunk-0 code for every full chunk
-//             (instruction-cache-resident code)
-//   9, 10     marginal LDS / VALU prices of the generated decode (rs_jit.h)
-//   11 lfix   every multiply-accumulate of the generated code reads the same
-//             low-nibble composite (one operand's data constant between
-//             consecutive instructions; same instruction count)
-//   12 lhfix  both composite operands fixed the same way
-#if defined(RSGPU_DIAG_CLOCK) && defined(RSGPU_DIAG_VARIANT)
-#define RSGPU_DIAG_VAR RSGPU_DIAG_VARIANT
-#else
-#define RSGPU_DIAG_VAR 0
-#endif
+// The timing-only energy variants (DIAG_VARIANT=n) are policies of their own:
+// kernel_hooks.h / diag_variants.h.
 
 #ifdef RSGPU_DIAG_CLOCK
 namespace rsgpu {
@@ -82,13 +57,18 @@ __device__ __forceinline__ unsigned long long memrealtime()
             s_[3] = r1_;                                                                            \
         }                                                                                           \
     } while (0)
-// variant 6: per-wave cycle sums per phase of the stamped workgroups
-#define RSGPU_DIAG_PHASE_TABLE \
-    static __device__ unsigned long long g_rsgpu_phase[::rsgpu::diag::kSlots][::rsgpu::diag::kPhaseWaves][::rsgpu::diag::kPhases];
+// variant 6: per-wave cycle sums per phase of the stamped workgroups (one
+// table per translation unit, as the clock table)
 namespace rsgpu {
 namespace diag {
 constexpr int kPhases = 8;
 constexpr int kPhaseWaves = 4;
+}  // namespace diag
+}  // namespace rsgpu
+static __device__ unsigned long long g_rsgpu_phase[::rsgpu::diag::kSlots][::rsgpu::diag::kPhaseWaves]
+                                                  [::rsgpu::diag::kPhases];
+namespace rsgpu {
+namespace diag {
 struct PhaseTimer {
     unsigned long long sum[kPhases] = {}, t, start;
     __device__ PhaseTimer() : t(memtime()), start(t) {}
@@ -98,14 +78,13 @@ struct PhaseTimer {
         sum[p] += n - t;
         t = n;
     }
-    template <class Table>
-    __device__ void end(Table& tab, int wave)
+    __device__ void end(int wave)
     {
         sum[kPhases - 1] = memtime() - start;
         const unsigned lin = blockIdx.x + gridDim.x * blockIdx.y;
         if ((threadIdx.x & 63) == 0 && lin % kEvery == 0 && wave < kPhaseWaves)
             for (int i = 0; i < kPhases; ++i)
-                tab[(lin / kEvery) % kSlots][wave][i] = sum[i];
+                g_rsgpu_phase[(lin / kEvery) % kSlots][wave][i] = sum[i];
     }
 };
 }  // namespace diag
@@ -134,7 +113,6 @@ struct PhaseTimer {
     }
 #else
 #define RSGPU_DIAG_TABLE
-#define RSGPU_DIAG_PHASE_TABLE
 #define RSGPU_DIAG_PHASE_READER(NAME)
 #define RSGPU_DIAG_BEGIN()
 #define RSGPU_DIAG_END() \
@@ -142,3 +120,14 @@ struct PhaseTimer {
     } while (0)
 #define RSGPU_DIAG_READER(NAME)
 #endif
+
+namespace rsgpu {
+namespace diag {
+// phase stamps of k_rs_jitw: the diagnostic PhaseTimer when the hooks ask
+// for them (variant 6), nothing otherwise
+struct NoPhases {
+    __device__ void mark(int) {}
+    __device__ void end(int) {}
+};
+}  // namespace diag
+}  // namespace rsgpu

@@ -41,6 +41,7 @@
 #include "bitslice.h"
 #include "diag_clock.h"
 #include "gf256.h"
+#include "kernel_hooks.h"
 #include "rs_kernels.h"
 
 namespace rsgpu {
@@ -195,9 +196,7 @@ template <class P, int K, int C, int R0, int NR, int PART>
 __device__ __forceinline__ void consume_part(uint32_t (&acc)[NR][8], uint32_t (&p0)[8], const uint4* buf,
                                              int lane, int j0)
 {
-#if RSGPU_DIAG_VAR == 3
-    uint32_t zp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-#endif
+    [[maybe_unused]] uint32_t zp[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // kernel_hooks.h kZeroValuPlanes only
     [&]<int... Ts>(std::integer_sequence<int, Ts...>) {
         (
             [&] {
@@ -206,16 +205,18 @@ __device__ __forceinline__ void consume_part(uint32_t (&acc)[NR][8], uint32_t (&
                     if (j0 + Ts < K) {
                         const uint4 u = buf[(Ts * 2 + 0) * 64 + lane];
                         const uint4 v = buf[(Ts * 2 + 1) * 64 + lane];
-#if RSGPU_DIAG_VAR == 3
-                        // diagnostic: the reads kept, the VALU fed zeros that are new
-                        // values to the compiler per source (no instruction, no CSE)
-                        asm volatile("" ::"v"(u.x), "v"(u.y), "v"(u.z), "v"(u.w), "v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w));
-                        asm volatile("" : "+v"(zp[0]), "+v"(zp[1]), "+v"(zp[2]), "+v"(zp[3]), "+v"(zp[4]),
-                                     "+v"(zp[5]), "+v"(zp[6]), "+v"(zp[7]));
-                        const uint32_t pl[8] = {zp[0], zp[1], zp[2], zp[3], zp[4], zp[5], zp[6], zp[7]};
-#else
-                        const uint32_t pl[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
-#endif
+                        uint32_t pl[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
+                        if constexpr (Hooks::kZeroValuPlanes) {
+                            // the reads kept, the VALU fed zeros that are new values to
+                            // the compiler per source (no instruction, no CSE)
+                            asm volatile("" ::"v"(u.x), "v"(u.y), "v"(u.z), "v"(u.w), "v"(v.x), "v"(v.y), "v"(v.z),
+                                         "v"(v.w));
+                            asm volatile("" : "+v"(zp[0]), "+v"(zp[1]), "+v"(zp[2]), "+v"(zp[3]), "+v"(zp[4]),
+                                         "+v"(zp[5]), "+v"(zp[6]), "+v"(zp[7]));
+#pragma unroll
+                            for (int a = 0; a < 8; ++a)
+                                pl[a] = zp[a];
+                        }
                         if constexpr (T == 0) {
 #pragma unroll
                             for (int a = 0; a < 8; ++a)
@@ -252,10 +253,10 @@ __device__ __forceinline__ void run_group(const Args& a, uint4 (*lds)[S * 2 * 64
     const bool inb = tp.inb;
     // source offset from the tile's first block; out-of-range lanes re-read
     // the row head
-    // diagnostic variant 1 (diag_clock.h): rows of blocks 0 and 1, 16 KB each
-    constexpr bool kWin = RSGPU_DIAG_VAR == 1;
-    const long long wo = kWin ? (long long)(blockIdx.x & 7) * 2048 + lane * 32 : tp.o;
-    const long long wb = kWin ? (tp.b0 & 1) : tp.b0;
+    // (kernel_hooks.h: the diagnostic HBM-quiet variant moves both into a
+    // two-block window)
+    const long long wo = Hooks::data_offset(tp.o, blockIdx.x, lane);
+    const long long wb = Hooks::data_block(tp.b0);
     const long long loff = inb ? tp.db * (long long)K * a.pitch + wo : 0;
     const uint8_t* sb = a.src + (size_t)wb * K * a.pitch;
     auto live = [&](int j) { return j < K; };
@@ -309,16 +310,10 @@ __device__ __forceinline__ void run_group(const Args& a, uint4 (*lds)[S * 2 * 64
                 uint4 u = buf[(t * 2 + 0) * 64 + lane];
                 uint4 v = buf[(t * 2 + 1) * 64 + lane];
                 uint32_t W[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
-                if constexpr (RSGPU_DIAG_VAR == 5)
-                    continue;  // diagnostic: raw bytes stay as the planes
+                if constexpr (!Hooks::kTransposes)
+                    continue;
                 tr8(W, m4, m2, m1);
-                if constexpr (RSGPU_DIAG_VAR == 2) {  // zero planes, the transpose kept
-                    asm volatile("" ::"v"(W[0]), "v"(W[1]), "v"(W[2]), "v"(W[3]), "v"(W[4]), "v"(W[5]),
-                                 "v"(W[6]), "v"(W[7]));
-#pragma unroll
-                    for (int i = 0; i < 8; ++i)
-                        W[i] = 0;
-                }
+                hook_planes<Hooks>(W);
                 buf[(t * 2 + 0) * 64 + lane] = make_uint4(W[0], W[1], W[2], W[3]);
                 buf[(t * 2 + 1) * 64 + lane] = make_uint4(W[4], W[5], W[6], W[7]);
             }

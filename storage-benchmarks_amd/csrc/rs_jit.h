@@ -35,26 +35,13 @@
 #pragma once
 #include <stdint.h>
 
-#if defined(__HIPCC__)
-#define RJ_HD __host__ __device__
-#else
-#define RJ_HD
-#endif
-
-// diagnostic energy variants (diag_clock.h): 3 lands the planes in dead
-// registers, 4 drops the per-source LDS wait; 0 in the product build
-#if defined(RSGPU_DIAG_CLOCK) && defined(RSGPU_DIAG_VARIANT)
-#define RSGPU_JIT_DIAG_VAR RSGPU_DIAG_VARIANT
-#else
-#define RSGPU_JIT_DIAG_VAR 0
-#endif
+#include "jit_enc.h"
+#include "kernel_hooks.h"
 
 namespace rsgpu {
 namespace jit {
 
 constexpr int ACC = 64;          // accumulator base register
-constexpr int LDS_SRC = 2048;    // LDS bytes per source: [2 halves][64 lanes] x 16 B
-constexpr int LDS_HALF = 1024;
 constexpr int PRO_BYTES = 16;
 constexpr int PRE_BYTES = 112;   // per source before the multiply-accumulates
 constexpr int EPI_BYTES = 8;
@@ -79,34 +66,6 @@ RJ_HD constexpr int table_reg(int bank, int hi, int n)
     const int below = 1 + (n > 2) + (n > 4) + (n > 8);
     return 32 + 11 * hi + (n - below - 1);
 }
-
-// ---- gfx950 encodings (llvm-mc -mcpu=gfx950 -show-encoding) -------------
-
-RJ_HD constexpr uint64_t enc_bitop3_96(int d, int a, int b, int c)  // d = a ^ b ^ c
-{
-    const uint32_t w0 = 0xd2340200u | (uint32_t)d;
-    const uint32_t w1 = 0xd0000000u | ((uint32_t)(256 + c) << 18) | ((uint32_t)(256 + b) << 9) |
-                        (uint32_t)(256 + a);
-    return (uint64_t)w1 << 32 | w0;
-}
-RJ_HD constexpr uint64_t enc_xor_e64(int d, int a, int b)  // VOP3 form, 8 bytes
-{
-    const uint32_t w0 = 0xd1150000u | (uint32_t)d;
-    const uint32_t w1 = ((uint32_t)(256 + b) << 9) | (uint32_t)(256 + a);
-    return (uint64_t)w1 << 32 | w0;
-}
-RJ_HD constexpr uint32_t enc_xor_e32(int d, int a, int b)  // VOP2, 4 bytes
-{
-    return 0x2a000000u | ((uint32_t)d << 17) | ((uint32_t)b << 9) | (uint32_t)(256 + a);
-}
-RJ_HD constexpr uint64_t enc_ds_read_b128(int vd, int vaddr, int offset)
-{
-    return (uint64_t)(((uint32_t)vd << 24) | (uint32_t)vaddr) << 32 | (0xd9fe0000u | (uint32_t)offset);
-}
-constexpr uint32_t S_NOP0 = 0xbf800000u;
-constexpr uint64_t NOP2 = (uint64_t)S_NOP0 << 32 | S_NOP0;  // two s_nop 0: a zero-mask word
-constexpr uint32_t S_SETPC_82 = 0xbe801d52u;  // s_setpc_b64 s[82:83]
-RJ_HD constexpr uint32_t enc_waitcnt_lgkm(int n) { return 0xbf8cc07fu | ((uint32_t)n << 8); }
 
 // Row b of the 8 x 8 GF(2) matrix of x -> c x: bit a set iff bit b of c 2^a.
 RJ_HD constexpr uint8_t mat_row(uint8_t c, int b)
@@ -235,9 +194,9 @@ template <int R_, int CS_>
 struct Wide {
     static constexpr int R = R_, CS = CS_;
     static constexpr int ADDR = 9, PL = 10, CL = 18, ACC = 40;
-    // bytes per source before the multiply-accumulates (diagnostic variants
-    // 9 / 10 add two LDS reads / eight VALU per source: marginal prices)
-    static constexpr int PRE = 112 + (RSGPU_JIT_DIAG_VAR == 9 ? 16 : RSGPU_JIT_DIAG_VAR == 10 ? 32 : 0);
+    // bytes per source before the multiply-accumulates (kernel_hooks.h: 112
+    // in the product)
+    static constexpr int PRE = 112 + Hooks::kPreExtra;
     RJ_HD static constexpr int src_bytes(int nslot) { return PRE + 64 * nslot; }
     RJ_HD static constexpr int chunk_stride() { return (CS * src_bytes(R) + 8 + 63) / 64 * 64; }
 
@@ -259,19 +218,10 @@ struct Wide {
     // accumulator acc is this base OR (acc << 32 | acc).
     RJ_HD static constexpr uint64_t mac_base(uint8_t m)
     {
-        const int lo = m & 15, hi = m >> 4;
-        // diagnostic variants 11 / 12 (diag_clock.h): operand data held
-        // constant between consecutive multiply-accumulates (timing only)
-        if constexpr (RSGPU_JIT_DIAG_VAR == 11 || RSGPU_JIT_DIAG_VAR == 12) {
-            const int l = 1, h = RSGPU_JIT_DIAG_VAR == 12 ? 1 : hi;
-            return lo && hi ? enc_bitop3_96(0, 0, treg(0, l), treg(1, h))
-                   : lo     ? enc_xor_e64(0, 0, treg(0, l))
-                   : hi     ? enc_xor_e64(0, 0, treg(1, h))
-                            : NOP2;
-        }
-        return lo && hi ? enc_bitop3_96(0, 0, treg(0, lo), treg(1, hi))
-               : lo     ? enc_xor_e64(0, 0, treg(0, lo))
-               : hi     ? enc_xor_e64(0, 0, treg(1, hi))
+        const int lo = m & 15, hi = m >> 4, l = Hooks::mac_lo(lo), h = Hooks::mac_hi(hi);
+        return lo && hi ? enc_bitop3_96(0, 0, treg(0, l), treg(1, h))
+               : lo     ? enc_xor_e64(0, 0, treg(0, l))
+               : hi     ? enc_xor_e64(0, 0, treg(1, h))
                         : NOP2;
     }
     RJ_HD static constexpr uint64_t with_acc(uint64_t base, int acc)
@@ -292,27 +242,15 @@ struct Wide {
     // 32-bit word i (< PRE / 4 = 28) of source t's preamble
     RJ_HD static constexpr uint32_t pre_u32(int t, int i)
     {
-        if constexpr (RSGPU_JIT_DIAG_VAR == 9) {  // the planes read a second time, into v18..v25
-            if (i >= 4 && i < 8) {
-                const uint64_t d = enc_ds_read_b128(i < 6 ? CL : CL + 4, ADDR, t * LDS_SRC + (i < 6 ? 0 : LDS_HALF));
-                return (i & 1) ? (uint32_t)(d >> 32) : (uint32_t)d;
-            }
-            if (i >= 8)
-                i -= 4;
-        }
-        if constexpr (RSGPU_JIT_DIAG_VAR == 10) {  // after the composites: v18..v21 ^= v10 twice
-            if (i >= 27 && i < 35)
-                return enc_xor_e32(CL + ((i - 27) >> 1), PL, CL + ((i - 27) >> 1));
-            if (i >= 35)
-                return S_NOP0;
-        }
+        if (uint32_t w = 0; Hooks::pre_word(t, i, PL, CL, ADDR, &w))
+            return w;
+        i = Hooks::pre_index(i);
         if (i < 4) {
-            constexpr int PLD = RSGPU_JIT_DIAG_VAR == 3 ? CL : PL;
-            const uint64_t d = enc_ds_read_b128(i < 2 ? PLD : PLD + 4, ADDR, t * LDS_SRC + (i < 2 ? 0 : LDS_HALF));
+            const uint64_t d = enc_ds_read_b128(i < 2 ? PL : PL + 4, ADDR, t * LDS_SRC + (i < 2 ? 0 : LDS_HALF));
             return (i & 1) ? (uint32_t)(d >> 32) : (uint32_t)d;
         }
         if (i == 4)
-            return RSGPU_JIT_DIAG_VAR == 4 ? S_NOP0 : enc_waitcnt_lgkm(0);
+            return enc_waitcnt_lgkm(0);
         const int j = i - 5;
         if (j >= 22)
             return S_NOP0;

@@ -23,6 +23,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <type_traits>
 #include <utility>
 
 #include "bitslice.h"
@@ -46,16 +47,12 @@ using bs::wait_vm;
 constexpr int C = 8;  // sources per LDS chunk (double-buffered)
 
 RSGPU_DIAG_TABLE
-RSGPU_DIAG_PHASE_TABLE
 
-// phase stamps of the diagnostic variant 6 (diag_clock.h); nothing otherwise
-struct NoPhases {
-    __device__ void mark(int) {}
-};
-#if RSGPU_DIAG_VAR == 6
-using JitwPhases = diag::PhaseTimer;
+// k_rs_jitw's phase stamps (the diagnostic build's variant 6, kernel_hooks.h)
+#ifdef RSGPU_DIAG_CLOCK
+using JitwPhases = std::conditional_t<Hooks::kPhaseStamps, diag::PhaseTimer, diag::NoPhases>;
 #else
-using JitwPhases = NoPhases;
+using JitwPhases = diag::NoPhases;
 #endif
 
 // Instrumentation points of k_rs_jit.  The product instantiates JitHooks:
@@ -302,16 +299,13 @@ __global__ __launch_bounds__(64 * NV * TPW) __attribute__((amdgpu_num_vgpr(40)))
         return;
     const int k = a.k;
     const int nch = (k + CS - 1) / CS;
-    // diagnostic variant 1 (diag_clock.h): rows of blocks 0 and 1, 16 KB each
-    const int bw = RSGPU_DIAG_VAR == 1 ? (b & 1) : b;
+    const int bw = (int)Hooks::data_block(b);
     const uint8_t* const* srcs = a.srcs + (size_t)bw * k;
     uint8_t* const* dsts = a.dsts + (size_t)bw * a.dst_stride;
-    // diagnostic variant 7: block 0's code for every block (L2-resident)
-    const uint8_t* code = a.code + (size_t)(RSGPU_DIAG_VAR == 7 ? 0 : b) * a.block_stride +
-                          (size_t)wave * nch * a.chunk_stride;
+    const uint8_t* code = a.code + (size_t)Hooks::code_block(b) * a.block_stride + (size_t)wave * nch * a.chunk_stride;
     const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint4*)&lds[0][tw][0];
     constexpr uint32_t kBuf = TPW * CS * 2 * 64 * 16;  // bytes between the two chunk buffers
-    const long long off = (RSGPU_DIAG_VAR == 1 ? (tile & 7) : tile) * 2048 + lane * 32;
+    const long long off = Hooks::data_offset(tile * 2048 + lane * 32, tile, lane);
     // lanes past the row end re-read its head (results never stored; at C4
     // 24 of 64 lanes of every row's last tile).  Loading nothing there cut
     // the C4 decode's HBM bytes but not its time (3.26-3.28 vs 3.26-3.27 ms
@@ -411,17 +405,11 @@ __global__ __launch_bounds__(64 * NV * TPW) __attribute__((amdgpu_num_vgpr(40)))
             // three -- the step unchanged in a same-process ABBA x10,
             // profiles/r05_energy/ab_knob_asm_transposes.json; not kept.)
             const uint32_t m4 = vconst(0x0F0F0F0Fu), m2 = vconst(0x33333333u), m1 = vconst(0x55555555u);
-            for (int t = wave; t < nt && RSGPU_DIAG_VAR != 5; t += NV) {
+            for (int t = wave; t < nt && Hooks::kTransposes; t += NV) {
                 uint4 u = buf[(t * 2 + 0) * 64 + lane], v = buf[(t * 2 + 1) * 64 + lane];
                 uint32_t Wd[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
                 tr8(Wd, m4, m2, m1);
-                if constexpr (RSGPU_DIAG_VAR == 2) {  // zero planes, the transpose kept
-                    asm volatile("" ::"v"(Wd[0]), "v"(Wd[1]), "v"(Wd[2]), "v"(Wd[3]), "v"(Wd[4]), "v"(Wd[5]),
-                                 "v"(Wd[6]), "v"(Wd[7]));
-#pragma unroll
-                    for (int i = 0; i < 8; ++i)
-                        Wd[i] = 0;
-                }
+                hook_planes<Hooks>(Wd);
                 buf[(t * 2 + 0) * 64 + lane] = make_uint4(Wd[0], Wd[1], Wd[2], Wd[3]);
                 buf[(t * 2 + 1) * 64 + lane] = make_uint4(Wd[4], Wd[5], Wd[6], Wd[7]);
             }
@@ -434,17 +422,12 @@ __global__ __launch_bounds__(64 * NV * TPW) __attribute__((amdgpu_num_vgpr(40)))
         ptrs(chunk_of(min(i + 2, nch - 1)), pn);  // in flight during this chunk's code
         ph.mark(4);  // phase 4: next chunk's LDS-DMA issue, row pointers
         const uint32_t la = lds0 + (uint32_t)(par * kBuf) + lane * 16;
-        // diagnostic variant 8: chunk 0's code for every full chunk (the
-        // wave's code stays in the instruction cache)
-        const uint8_t* fn = code + (size_t)(RSGPU_DIAG_VAR == 8 && nt == CS ? 0 : ch) * a.chunk_stride;
-        if constexpr (RSGPU_DIAG_VAR == 3 && R == 16)  // zero planes; the LDS reads land in v18..v25
+        const uint8_t* fn = code + (size_t)Hooks::code_chunk(ch, nt == CS) * a.chunk_stride;
+        if constexpr (Hooks::kZeroValuPlanes)  // the diagnostic build's variant 3 (kernel_hooks.h)
             asm volatile("v_mov_b32 v10, 0\n v_mov_b32 v11, 0\n v_mov_b32 v12, 0\n v_mov_b32 v13, 0\n"
-                         " v_mov_b32 v14, 0\n v_mov_b32 v15, 0\n v_mov_b32 v16, 0\n v_mov_b32 v17, 0\n"
-                         " s_swappc_b64 s[82:83], %[fn]"
-                         :
-                         : [fn] "s"(fn), "{v9}"(la)
-                         : RSGPU_JW_CALL_CLOBBERS, "s82", "s83", "scc", "memory", RSGPU_J16_ACC_CLOBBERS);
-        else if constexpr (R == 16)
+                         " v_mov_b32 v14, 0\n v_mov_b32 v15, 0\n v_mov_b32 v16, 0\n v_mov_b32 v17, 0"
+                         ::: "v10", "v11", "v12", "v13", "v14", "v15", "v16", "v17");
+        if constexpr (R == 16)
             asm volatile("s_swappc_b64 s[82:83], %[fn]"
                          :
                          : [fn] "s"(fn), "{v9}"(la)
@@ -484,9 +467,7 @@ __global__ __launch_bounds__(64 * NV * TPW) __attribute__((amdgpu_num_vgpr(40)))
         }(std::make_integer_sequence<int, R>{});
     }
     ph.mark(6);  // phase 6: output transposes and stores
-#if RSGPU_DIAG_VAR == 6
-    ph.end(g_rsgpu_phase, wv);
-#endif
+    ph.end(wv);
     RSGPU_DIAG_END();
 }
 

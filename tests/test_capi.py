@@ -107,3 +107,25 @@ def test_erasure_patterns_match_definition():
 def test_erasure_patterns_rejects_bad_args():
     with pytest.raises(rsgpu.RsGpuError):
         rsgpu.erasure_patterns(1, 0, 1, 4, 5)
+
+
+def test_diagnostic_variants_need_the_diagnostic_build():
+    """the timing-only variants (csrc/diag_variants.h,
+    wrong outputs by design) enter a kernel only through kernel_hooks.h, and a
+    stray -DRSGPU_DIAG_VARIANT without the diagnostic library's own flag
+    (RSGPU_DIAG_CLOCK, `make diag`) does not compile; the product kernels
+    name no variant."""
+    csrc = os.path.join(ROOT, "storage-benchmarks_amd", "csrc")
+    src = '#include "kernel_hooks.h"\nint main() { return rsgpu::Hooks::kVariant; }\n'
+    r = subprocess.run(["g++", "-std=c++20", "-fsyntax-only", "-I", csrc, "-DRSGPU_DIAG_VARIANT=3", "-x", "c++",
+                        "-"], input=src, capture_output=True, text=True)
+    assert r.returncode != 0 and "only the diagnostic library" in r.stderr, r.stderr
+    r = subprocess.run(["g++", "-std=c++20", "-fsyntax-only", "-I", csrc, "-DRSGPU_DIAG_VARIANT=3",
+                        "-DRSGPU_DIAG_CLOCK", "-x", "c++", "-"], input=src, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    for f in ("rs_jit.hip", "rs_bitsliced.hip", "rs_jit.h"):
+        text = open(os.path.join(csrc, f)).read()
+        assert "RSGPU_DIAG_VAR" not in text and "DIAG_VARIANT" not in text, f
+    mk = open(os.path.join(ROOT, "storage-benchmarks_amd", "Makefile")).read()
+    product_flags = mk.split("HIPFLAGS ?=")[1].splitlines()[0]
+    assert "DIAG" not in product_flags
