@@ -325,6 +325,9 @@ __global__ __launch_bounds__(64 * NV * TPW) __attribute__((amdgpu_num_vgpr(40)))
         for (int i = 0; i < PW; ++i)
             p[i] = csrcs[c0 + min(wave + NV * i, nt - 1)];  // in bounds, unconditional
     };
+    // NOTE: the first word of chunk buffer 1 carries the chunk rotation
+    // (below) until every wave has read it, before the first chunk barrier:
+    // no LDS-DMA may target buffer 1 (par 1) before that barrier.
     auto issue = [&](int ch, int par, const uint8_t* const (&p)[PW]) {
         const int c0 = ch * CS, nt = min(CS, k - c0);
         const uint32_t base = lds0 + (uint32_t)(par * kBuf);

@@ -995,21 +995,32 @@ def test_wide_rows_decode_in_at_most_two_launches(ctx, k, e, L):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("prefetch", [-1, 1])
 @pytest.mark.parametrize("period", [600, 1, 37, 0])
 @pytest.mark.parametrize("k,e,L,B", [(64, 32, 1000000, 2), (64, 32, 32000, 9), (100, 20, 6144, 3),
                                      (64, 40, 65536, 3), (150, 100, 16384, 2), (18, 17, 4096, 3)])
-def test_jitw_chunk_rotation(ctx, period, k, e, L, B):
+def test_jitw_chunk_rotation(ctx, period, prefetch, k, e, L, B):
     """k_rs_jitw's chunk order rotated by the workgroup's start time, for
     periods that put neighbouring workgroups in different phases (1 tick) and
     for none (0):
     every chunk applied exactly once, so the same recovered bytes with the
     erased rows poisoned -- two- and four-wave layouts, passes above 64 rows,
-    and a three-chunk block whose last chunk is partial (k 18, CS 5)."""
+    and a four-chunk block whose last chunk is partial (k 18, CS 5: 5 + 5 +
+    5 + 3).  Both users of the kernel rotate: the per-block decode and the
+    GENERATED encode's shared program (its parity feeds the decode, so a
+    wrong parity shows as wrong recovered bytes).  prefetch 1 turns the
+    short-row code prefetch on beside the rotation (the rotation's broadcast
+    word lives in chunk buffer 1, which no LDS-DMA may write before the first
+    chunk barrier)."""
     import ctypes
     f_rot = rsgpu.testhooks().rsgpu_internal_set_jitw_rot
     f_rot.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    f_pf = rsgpu.testhooks().rsgpu_internal_set_jitw_prefetch
+    f_pf.argtypes = [ctypes.c_void_p, ctypes.c_int]
     ctx.set_decode_kernel("generated")
+    ctx.set_encode_kernel("generated")
     assert f_rot(ctx._h, period) == 0
+    assert f_pf(ctx._h, prefetch) == 0
     try:
         enc = rsgpu.GpuEncoder(k, L, e, blocks=B, seed=79, ctx=ctx)
         enc.encode_all()
@@ -1017,4 +1028,6 @@ def test_jitw_chunk_rotation(ctx, period, k, e, L, B):
         assert decode_poisoned(ctx, enc, dec)
     finally:
         f_rot(ctx._h, -1)
+        f_pf(ctx._h, -1)
+        ctx.set_encode_kernel("auto")
         ctx.set_decode_kernel("auto")
