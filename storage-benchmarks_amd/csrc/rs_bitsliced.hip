@@ -147,6 +147,7 @@ struct Args {
     long long pitch, len;
     long long blocks;     // B
     int flat;             // tiles over the blocks' rows laid end to end (short rows)
+    int prio;             // A/B: wave priority level from the transposes to the part barrier
 };
 
 // Where lane `lane` of column tile `tile` works: the tile's first block b0,
@@ -305,6 +306,12 @@ __device__ __forceinline__ void run_group(const Args& a, uint4 (*lds)[S * 2 * 64
         } else {
             bs::wait_vm(0);
         }
+        if (a.prio == 1)
+            asm volatile("s_setprio 1" ::: "memory");
+        else if (a.prio == 2)
+            asm volatile("s_setprio 2" ::: "memory");
+        else if (a.prio == 3)
+            asm volatile("s_setprio 3" ::: "memory");
         for (int t = G; t < nt; t += NW)
             if (live(j0 + t)) {
                 uint4 u = buf[(t * 2 + 0) * 64 + lane];
@@ -318,6 +325,8 @@ __device__ __forceinline__ void run_group(const Args& a, uint4 (*lds)[S * 2 * 64
                 buf[(t * 2 + 1) * 64 + lane] = make_uint4(W[4], W[5], W[6], W[7]);
             }
         bs::barrier_lds();
+        if (a.prio)
+            asm volatile("s_setprio 0" ::: "memory");
         const int part = n % NP;
         if (part == 0 && n != 0)
             twiddle_rows<P, R0, NR>(acc, std::make_integer_sequence<int, NR>{});
@@ -670,7 +679,7 @@ hipError_t launch_syn(const SynArgs& a, long long blocks, hipStream_t st)
 
 template <int K, int E, int C, int NW>
 hipError_t launch(const uint8_t* src, uint8_t* out, long long pitch, long long len,
-                  long long blocks, hipStream_t st)
+                  long long blocks, hipStream_t st, int prio)
 {
     // short rows whose last tile is partial: tiles over the rows of all
     // blocks end to end (tile_pos).  A lane addresses its rows from the
@@ -678,7 +687,7 @@ hipError_t launch(const uint8_t* src, uint8_t* out, long long pitch, long long l
     // pitch + o, db <= 2048 / len + 1, must stay below 2^32
     const bool flat = blocks > 1 && len % 2048 != 0 && len < 65536 && pitch % 32 == 0 &&
                       (unsigned long long)(2048 / len + 2) * K * (unsigned long long)pitch < (1ull << 32);
-    Args a{src, out, pitch, len, blocks, flat ? 1 : 0};
+    Args a{src, out, pitch, len, blocks, flat ? 1 : 0, prio};
     dim3 grid(flat ? (unsigned)((blocks * len + 2047) / 2048) : (unsigned)((len + 2047) / 2048),
               flat ? 1u : (unsigned)blocks);
     hipLaunchKernelGGL((k_rs_bs<K, E, C, NW>), grid, dim3(64 * NW), 0, st, a);
@@ -733,15 +742,15 @@ hipError_t launch_rs_syn_split(int k, int e, const SynArgs& a, long long blocks,
 }
 
 hipError_t launch_rs_bitsliced(int k, int e, const uint8_t* src, uint8_t* out, long long pitch,
-                               long long len, long long blocks, hipStream_t st)
+                               long long len, long long blocks, hipStream_t st, int prio)
 {
-    if (k == 16 && e == 4) return bs::launch<16, 4, 16, 1>(src, out, pitch, len, blocks, st);
-    if (k == 16 && e == 8) return bs::launch<16, 8, 16, 1>(src, out, pitch, len, blocks, st);
-    if (k == 64 && e == 32) return bs::launch<64, 32, 16, 4>(src, out, pitch, len, blocks, st);
-    if (k == 64 && e == 16) return bs::launch<64, 16, 16, 2>(src, out, pitch, len, blocks, st);
-    if (k == 100 && e == 20) return bs::launch<100, 20, 20, 4>(src, out, pitch, len, blocks, st);
-    if (k == 5 && e == 4) return bs::launch<5, 4, 5, 1>(src, out, pitch, len, blocks, st);
-    if (k == 20 && e == 7) return bs::launch<20, 7, 20, 1>(src, out, pitch, len, blocks, st);
+    if (k == 16 && e == 4) return bs::launch<16, 4, 16, 1>(src, out, pitch, len, blocks, st, prio);
+    if (k == 16 && e == 8) return bs::launch<16, 8, 16, 1>(src, out, pitch, len, blocks, st, prio);
+    if (k == 64 && e == 32) return bs::launch<64, 32, 16, 4>(src, out, pitch, len, blocks, st, prio);
+    if (k == 64 && e == 16) return bs::launch<64, 16, 16, 2>(src, out, pitch, len, blocks, st, prio);
+    if (k == 100 && e == 20) return bs::launch<100, 20, 20, 4>(src, out, pitch, len, blocks, st, prio);
+    if (k == 5 && e == 4) return bs::launch<5, 4, 5, 1>(src, out, pitch, len, blocks, st, prio);
+    if (k == 20 && e == 7) return bs::launch<20, 7, 20, 1>(src, out, pitch, len, blocks, st, prio);
     return hipErrorInvalidValue;
 }
 

@@ -166,6 +166,8 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_num_vgpr(64))) void 
         uint4* buf = lds[ch & 1];
         wait_vm(0);  // this chunk's own sources, issued behind the previous barrier
         jp.mark(0);
+        if (a.prio)  // the transposes up to the barrier over other waves' code (as k_rs_jitw)
+            asm volatile("s_setprio 2" ::: "memory");
         // own share of this chunk: bytes -> bit-planes, in place, two
         // sources at a time (both sets of LDS reads in flight together)
         int t = wave;
@@ -192,6 +194,8 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_num_vgpr(64))) void 
         }
         jp.mark(1);
         barrier_lds();
+        if (a.prio)
+            asm volatile("s_setprio 0" ::: "memory");
         jp.mark(2);
         // one barrier per chunk: every wave is past its call of chunk ch - 1,
         // which read buffer (ch + 1) & 1, so chunk ch + 1 may land there now
@@ -349,6 +353,20 @@ __global__ __launch_bounds__(64 * NV * TPW) __attribute__((amdgpu_num_vgpr(40)))
     else
         asm volatile(RSGPU_J10_ZERO ::: RSGPU_J10_ACC_CLOBBERS);
     JitwPhases ph;
+    // Wave priority: a wave's transposes up to the chunk barrier run at a.prio
+    // (default 2) over the other waves' generated code, so the workgroup's
+    // last wave reaches the barrier sooner (same process ABBA, round 6,
+    // profiles/r06_prio/: C3 decode -2.5 %, C4 slices -2 %, C5 -2.4 %)
+    auto setprio = [](int lv) {
+        if (lv == 3)
+            asm volatile("s_setprio 3" ::: "memory");
+        else if (lv == 2)
+            asm volatile("s_setprio 2" ::: "memory");
+        else if (lv == 1)
+            asm volatile("s_setprio 1" ::: "memory");
+        else
+            asm volatile("s_setprio 0" ::: "memory");
+    };
     // The chunks' order is free (each chunk's code only adds into the
     // accumulators).  A rotation by the time the workgroup starts, chunk
     // (t / kRot) % nch first, keeps the workgroups that share a CU pair's
@@ -402,6 +420,8 @@ __global__ __launch_bounds__(64 * NV * TPW) __attribute__((amdgpu_num_vgpr(40)))
         ph.mark(0);  // phase 0: the previous call's return .. here (loop overhead, start)
         wait_vm(0);
         ph.mark(1);  // phase 1: this chunk's LDS-DMA
+        if (a.prio)
+            setprio(a.prio);
         {
             // (Tried, round 5: the wave's three sources' LDS reads batched in
             // hand-allocated asm, one exposed LDS latency per chunk instead of
@@ -420,6 +440,8 @@ __global__ __launch_bounds__(64 * NV * TPW) __attribute__((amdgpu_num_vgpr(40)))
         ph.mark(2);  // phase 2: transposes
         barrier_lds();
         ph.mark(3);  // phase 3: the chunk barrier
+        if (a.prio)
+            setprio(0);
         if (i + 1 < nch)
             issue(chunk_of(i + 1), par ^ 1, pn);
         ptrs(chunk_of(min(i + 2, nch - 1)), pn);  // in flight during this chunk's code

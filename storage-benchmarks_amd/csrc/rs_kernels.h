@@ -69,7 +69,7 @@ bool rs_bitsliced_available(int k, int e);
 // source are built per this many rows), 0 if none is compiled for (k, e)
 int rs_bitsliced_rows_per_wave(int k, int e);
 hipError_t launch_rs_bitsliced(int k, int e, const uint8_t* src, uint8_t* out, long long pitch,
-                               long long len, long long blocks, hipStream_t st);
+                               long long len, long long blocks, hipStream_t st, int prio = 0);
 // Small batches of the single-chunk codes (16,4) (16,8) (5,4) (20,7): four
 // waves per tile split the sources (k_rs_bs_split), same bytes.
 bool rs_bitsliced_split_available(int k, int e);
@@ -119,6 +119,7 @@ struct JitArgs {
     int code_prefetch = 0;           // k_rs_jitw: workgroups pull their block's code into L2 first
     int chunk_rot_ticks = 0;         // k_rs_jitw: > 0 rotates the chunk order by the start time
                                      // (s_memrealtime / chunk_rot_ticks), 0 = chunks in order
+    int prio = 0;                    // k_rs_jitw / k_rs_jit: wave priority from transposes to barrier
 };
 // k_rs_jitw's chunk rotation period for `rows` rows at k sources: about one
 // chunk's duration in 100 MHz ticks (measured best at 600 for C3's 16 rows)

@@ -386,6 +386,7 @@ int shared_program_launch(rsgpu_ctx* ctx, const uint8_t* coef, int k, int rows, 
             // -> 12.37 ms, step -2.7 %; (48, 24) step -0.7 %; C3's generated
             // encode 22.65 -> 21.73 ms, still 1.7 % behind k_rs_bs)
             j.chunk_rot_ticks = ctx->jitw_rot >= 0 ? ctx->jitw_rot : jitw_rot_ticks(j.rows);
+            j.prio = ctx->jitw_prio;
             KTimer kt(ctx, name, (size_t)blocks);
             RS_HIP(ctx, launch_rs_jitw(j, blocks, ctx->stream));
         }
@@ -404,6 +405,7 @@ int shared_program_launch(rsgpu_ctx* ctx, const uint8_t* coef, int k, int rows, 
         j.dst_stride = rows;
         j.len = len;
         j.status = nullptr;
+        j.prio = ctx->jitw_prio;
         KTimer kt(ctx, name, (size_t)blocks);
         RS_HIP(ctx, launch_rs_jit(j, blocks, ctx->stream));
     }
@@ -990,7 +992,7 @@ int rsgpu_encode_blocks(rsgpu_ctx* ctx, int k, int e, size_t len, size_t pitch, 
     if (compiled_ok && compiled_pays && !coef && aligned && len % 32 == 0 && rs_bitsliced_available(k, e)) {
         KTimer kt(ctx, "k_rs_bs(encode)", blocks);
         RS_HIP(ctx, launch_rs_bitsliced(k, e, d_src, d_parity, (long long)pitch, (long long)len,
-                                        (long long)blocks, ctx->stream));
+                                        (long long)blocks, ctx->stream, ctx->bs_prio));
         return RSGPU_OK;
     }
     if (compiled_ok && !coef && aligned && len % 4 == 0 && len % 32 != 0 &&
@@ -1236,6 +1238,7 @@ int jitw_launch(rsgpu_ctx* ctx, int k, int e, size_t len, size_t blocks, const u
         // workgroups run its code once each, and the rotation measured +0.5 %
         // on the C4 step (same-process ABBA x6, profiles/r05_rot/shared/)
         j.chunk_rot_ticks = ctx->jitw_rot >= 0 ? ctx->jitw_rot : j.code_prefetch ? 0 : jitw_rot_ticks(rows);
+        j.prio = ctx->jitw_prio;
         const int r = jitw_rows(rows);
         KTimer kt(ctx,
                   e > 64  ? "k_rs_jitw_passes(decode)"
@@ -1283,6 +1286,7 @@ int jit_decode_launch(rsgpu_ctx* ctx, int k, int e, size_t len, size_t blocks, c
         j.status = d_status;
         // few tiles per block: keep each block's code in one XCD's L2
         j.xcd_order = (len + 2047) / 2048 < kJitXcdTiles;
+        j.prio = ctx->jitw_prio;
         KTimer kt(ctx, "k_rs_jit(decode)", blocks);
         RS_HIP(ctx, launch_rs_jit(j, (long long)blocks, ctx->stream));
     }

@@ -28,6 +28,10 @@ struct rsgpu_ctx {
     int jitw_tpw = 0;  // k_rs_jitw column tiles per workgroup (0: by geometry)
     int jitw_prefetch = -1;  // k_rs_jitw code prefetch into L2 (-1: by geometry)
     int jitw_rot = -1;       // k_rs_jitw chunk rotation period, ticks (-1: by geometry, 0: off)
+    // wave priority of k_rs_bs / k_rs_jitw / k_rs_jit from a chunk's transposes
+    // to its barrier (0: off, the A/B hooks set it)
+    int bs_prio = 2;
+    int jitw_prio = 2;
     // short-row generated decode: prepare + emission on `aux` beside the
     // decode, in decode_pipe slices (-1: by geometry, 0 / 1: off)
     int decode_pipe = -1;

@@ -81,6 +81,28 @@ int rsgpu_internal_set_jitw_rot(rsgpu_ctx* ctx, int n)
     return RSGPU_OK;
 }
 
+// A-B hook (not part of include/rsgpu.h): the generated-code kernels
+// (k_rs_jitw, k_rs_jit) raise their waves' priority to level n from the
+// transposes to the chunk barrier (0: off; default 2).
+int rsgpu_internal_set_jitw_prio(rsgpu_ctx* ctx, int n)
+{
+    if (!ctx || n < 0 || n > 3)
+        return RSGPU_ERR_ARG;
+    ctx->jitw_prio = n;
+    return RSGPU_OK;
+}
+
+// A-B hook (not part of include/rsgpu.h): k_rs_bs raises its waves'
+// priority to level n from the transposes to the part barrier (0: off;
+// default 2).
+int rsgpu_internal_set_bs_prio(rsgpu_ctx* ctx, int n)
+{
+    if (!ctx || n < 0 || n > 3)
+        return RSGPU_ERR_ARG;
+    ctx->bs_prio = n;
+    return RSGPU_OK;
+}
+
 // Test / A-B hook (not part of include/rsgpu.h): slices of the short-row
 // generated decode whose prepare and emission run beside the decode
 // (rsgpu_decode_blocks; 0 or 1 off, -1 the library's choice).

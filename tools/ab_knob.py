@@ -64,9 +64,11 @@ def main() -> int:
         elif args.knob == "decode_kernel":
             ctx.set_decode_kernel(v)
         else:
-            f = getattr(rsgpu.testhooks(), args.knob)
-            f.argtypes = [ctypes.c_void_p, ctypes.c_int]
-            assert f(ctx._h, int(v)) == 0, (args.knob, v)
+            # several knobs at once: --knob a+b --values 0+0,2+2
+            for kn, kv in zip(args.knob.split("+"), v.split("+")):
+                f = getattr(rsgpu.testhooks(), kn)
+                f.argtypes = [ctypes.c_void_p, ctypes.c_int]
+                assert f(ctx._h, int(kv)) == 0, (kn, kv)
 
     def step():
         enc.encode_all()
