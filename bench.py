@@ -85,10 +85,10 @@ def parse(argv=None):
     p.add_argument("--no-verify", action="store_true")
     p.add_argument("--host-io", type=int, default=0, metavar="BLOCKS",
                    help="also time the host-resident path (H2D + kernel + D2H) on BLOCKS blocks")
-    p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r05_head", "traffic.json"),
+    p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r06_head", "traffic.json"),
                    help="JSON with PMC-derived HBM bytes per launch of the same workload "
                         "(tools/profile_round.sh)")
-    p.add_argument("--sq-counters", default=os.path.join(ROOT, "profiles", "r05_head", "sq_summary.txt"),
+    p.add_argument("--sq-counters", default=os.path.join(ROOT, "profiles", "r06_head", "sq_summary.txt"),
                    help="SQ counter summary of the same workload (tools/pmc_sq.sh + "
                         "tools/pmc_summary.py): VALU-issue roofline of each kernel")
     p.add_argument("--valu-ceiling", default=os.path.join(ROOT, "profiles", "r03_valu_ceiling.json"),
