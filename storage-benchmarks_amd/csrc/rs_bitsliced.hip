@@ -238,7 +238,7 @@ __device__ __forceinline__ void consume_part(uint32_t (&acc)[NR][8], uint32_t (&
 // chunk by chunk (Horner order, last chunk first) through the LDS parts:
 // while part n is transposed in place and consumed, part n+1 is already in
 // flight by LDS-DMA (global_load_lds_dwordx4, counted vmcnt, raw barriers).
-template <int K, int E, int C, int NW, int G>
+template <int K, int E, int C, int NW, int G, bool PRIO>
 __device__ __forceinline__ void run_group(const Args& a, uint4 (*lds)[S * 2 * 64])
 {
     using P = PlanHolder<K, E, C>;
@@ -306,12 +306,10 @@ __device__ __forceinline__ void run_group(const Args& a, uint4 (*lds)[S * 2 * 64
         } else {
             bs::wait_vm(0);
         }
-        if (a.prio == 1)
-            asm volatile("s_setprio 1" ::: "memory");
-        else if (a.prio == 2)
+        // the transposes up to the part barrier over the other workgroups'
+        // multiply-accumulates (round 6, profiles/r06_prio/: encode -1.2 to -2.3 %)
+        if constexpr (PRIO)
             asm volatile("s_setprio 2" ::: "memory");
-        else if (a.prio == 3)
-            asm volatile("s_setprio 3" ::: "memory");
         for (int t = G; t < nt; t += NW)
             if (live(j0 + t)) {
                 uint4 u = buf[(t * 2 + 0) * 64 + lane];
@@ -325,7 +323,7 @@ __device__ __forceinline__ void run_group(const Args& a, uint4 (*lds)[S * 2 * 64
                 buf[(t * 2 + 1) * 64 + lane] = make_uint4(W[4], W[5], W[6], W[7]);
             }
         bs::barrier_lds();
-        if (a.prio)
+        if constexpr (PRIO)
             asm volatile("s_setprio 0" ::: "memory");
         const int part = n % NP;
         if (part == 0 && n != 0)
@@ -364,14 +362,14 @@ constexpr int bs_waves_per_simd()
     return (E + NW - 1) / NW > 8 ? 2 : 16 / NW;
 }
 
-template <int K, int E, int C, int NW>
+template <int K, int E, int C, int NW, bool PRIO = true>
 __global__ __launch_bounds__(64 * NW, (bs_waves_per_simd<E, NW>())) void k_rs_bs(Args a)
 {
     __shared__ uint4 lds[2][S * 2 * 64];
     RSGPU_DIAG_BEGIN()
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     [&]<int... Gs>(std::integer_sequence<int, Gs...>) {
-        ((wave == Gs ? run_group<K, E, C, NW, Gs>(a, lds) : void()), ...);
+        ((wave == Gs ? run_group<K, E, C, NW, Gs, PRIO>(a, lds) : void()), ...);
     }(std::make_integer_sequence<int, NW>{});
     RSGPU_DIAG_END();
 }
@@ -690,7 +688,10 @@ hipError_t launch(const uint8_t* src, uint8_t* out, long long pitch, long long l
     Args a{src, out, pitch, len, blocks, flat ? 1 : 0, prio};
     dim3 grid(flat ? (unsigned)((blocks * len + 2047) / 2048) : (unsigned)((len + 2047) / 2048),
               flat ? 1u : (unsigned)blocks);
-    hipLaunchKernelGGL((k_rs_bs<K, E, C, NW>), grid, dim3(64 * NW), 0, st, a);
+    if (prio)
+        hipLaunchKernelGGL((k_rs_bs<K, E, C, NW, true>), grid, dim3(64 * NW), 0, st, a);
+    else
+        hipLaunchKernelGGL((k_rs_bs<K, E, C, NW, false>), grid, dim3(64 * NW), 0, st, a);
     return hipGetLastError();
 }
 

@@ -353,20 +353,10 @@ __global__ __launch_bounds__(64 * NV * TPW) __attribute__((amdgpu_num_vgpr(40)))
     else
         asm volatile(RSGPU_J10_ZERO ::: RSGPU_J10_ACC_CLOBBERS);
     JitwPhases ph;
-    // Wave priority: a wave's transposes up to the chunk barrier run at a.prio
-    // (default 2) over the other waves' generated code, so the workgroup's
-    // last wave reaches the barrier sooner (same process ABBA, round 6,
-    // profiles/r06_prio/: C3 decode -2.5 %, C4 slices -2 %, C5 -2.4 %)
-    auto setprio = [](int lv) {
-        if (lv == 3)
-            asm volatile("s_setprio 3" ::: "memory");
-        else if (lv == 2)
-            asm volatile("s_setprio 2" ::: "memory");
-        else if (lv == 1)
-            asm volatile("s_setprio 1" ::: "memory");
-        else
-            asm volatile("s_setprio 0" ::: "memory");
-    };
+    // Wave priority: a wave's transposes up to the chunk barrier run at level
+    // 2 (a.prio != 0, the default) over the other waves' generated code, so
+    // the workgroup's last wave reaches the barrier sooner (same process ABBA,
+    // round 6, profiles/r06_prio/: C3 decode -2.5 %, C4 slices -2 %, C5 -2.4 %)
     // The chunks' order is free (each chunk's code only adds into the
     // accumulators).  A rotation by the time the workgroup starts, chunk
     // (t / kRot) % nch first, keeps the workgroups that share a CU pair's
@@ -421,7 +411,7 @@ __global__ __launch_bounds__(64 * NV * TPW) __attribute__((amdgpu_num_vgpr(40)))
         wait_vm(0);
         ph.mark(1);  // phase 1: this chunk's LDS-DMA
         if (a.prio)
-            setprio(a.prio);
+            asm volatile("s_setprio 2" ::: "memory");
         {
             // (Tried, round 5: the wave's three sources' LDS reads batched in
             // hand-allocated asm, one exposed LDS latency per chunk instead of
@@ -441,7 +431,7 @@ __global__ __launch_bounds__(64 * NV * TPW) __attribute__((amdgpu_num_vgpr(40)))
         barrier_lds();
         ph.mark(3);  // phase 3: the chunk barrier
         if (a.prio)
-            setprio(0);
+            asm volatile("s_setprio 0" ::: "memory");
         if (i + 1 < nch)
             issue(chunk_of(i + 1), par ^ 1, pn);
         ptrs(chunk_of(min(i + 2, nch - 1)), pn);  // in flight during this chunk's code

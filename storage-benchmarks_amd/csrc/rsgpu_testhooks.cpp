@@ -82,8 +82,8 @@ int rsgpu_internal_set_jitw_rot(rsgpu_ctx* ctx, int n)
 }
 
 // A-B hook (not part of include/rsgpu.h): the generated-code kernels
-// (k_rs_jitw, k_rs_jit) raise their waves' priority to level n from the
-// transposes to the chunk barrier (0: off; default 2).
+// (k_rs_jitw, k_rs_jit) raise their waves' priority (to level 2) from the
+// transposes to the chunk barrier (n != 0, the default 2) or not (0).
 int rsgpu_internal_set_jitw_prio(rsgpu_ctx* ctx, int n)
 {
     if (!ctx || n < 0 || n > 3)
@@ -93,8 +93,8 @@ int rsgpu_internal_set_jitw_prio(rsgpu_ctx* ctx, int n)
 }
 
 // A-B hook (not part of include/rsgpu.h): k_rs_bs raises its waves'
-// priority to level n from the transposes to the part barrier (0: off;
-// default 2).
+// priority (to level 2) from the transposes to the part barrier (n != 0, the
+// default 2; its own instantiation) or not (0).
 int rsgpu_internal_set_bs_prio(rsgpu_ctx* ctx, int n)
 {
     if (!ctx || n < 0 || n > 3)
