@@ -1,5 +1,6 @@
 # Round 6 check of a build: the GPU suite, smoke, the driver's default bench
-# line, C4 and the diagnostic build's phase stamps (the hooks refactor).
+# line and C4.  (Round 6's first run also took the diagnostic build's phase
+# stamps at C4 after the hooks refactor: profiles/r06_check1/.)
 #   gpurun -- bash tools/r06_check.sh NAME  -> gpurun_out/NAME/
 set -o pipefail
 O=gpurun_out/${1:-r06_check}; mkdir -p $O
@@ -8,7 +9,6 @@ timeout -k 10 900 python3 -u -m pytest tests -x -q -m gpu --timeout 120 --timeou
 timeout -k 10 300 python3 -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 &&
 timeout -k 10 300 python3 -u bench.py > $O/bench_default.log 2>&1 &&
 timeout -k 10 300 python3 -u bench.py --config c4 --no-cpu-baseline > $O/c4.log 2>&1 &&
-RSGPU_LIB=tools/diag/librsgpu_diag_v6.so timeout -k 10 120 python3 -u tools/bound_probe.py --symbol-size 32000 --blocks 4096 --seconds 1.5 --order dec:rand --out $O/phases_v6_c4.json > $O/phases_v6_c4.log 2>&1 &&
 tail -1 $O/pytest_gpu.log && tail -c 600 $O/bench_default.log && python3 -c "
 import json
 for f in ('bench_default', 'c4'):
