@@ -38,6 +38,7 @@ import json
 import math
 import os
 import shutil
+import signal
 import socket
 import statistics
 import subprocess
@@ -101,6 +102,9 @@ def parse(argv=None):
     p.add_argument("--dist-backend", default="gloo", choices=["gloo", "nccl"])
     p.add_argument("--dist-timeout", type=float, default=900.0,
                    help="seconds a collective waits for the other ranks")
+    # tests only: this rank fails right after the process group is up, the
+    # others wait in a barrier (the failure path of a multi-rank run)
+    p.add_argument("--fail-rank", type=int, default=None, help=argparse.SUPPRESS)
     return p.parse_args(argv)
 
 
@@ -856,6 +860,8 @@ def report_failure(args, rank, world, store, ex, wait_s=10.0):
     """A rank's exception: its record goes to the process group's store; rank
     0 gathers every rank's record and prints the run's one JSON line.
     Returns (exit status, the line or None)."""
+    if world > 1:  # the launcher's stop signal must not cut the report short
+        signal.signal(signal.SIGTERM, signal.SIG_IGN)
     rec = failure_record(rank, ex)
     print(f"bench.py rank {rank}: {rec['error']}\n{rec['where']}", file=sys.stderr, flush=True)
     if store is not None:
@@ -869,6 +875,14 @@ def report_failure(args, rank, world, store, ex, wait_s=10.0):
     line = failure_line(args, world, failed)
     print(json.dumps(line), flush=True)
     return 1, line
+
+
+class RankStopped(Exception):
+    """The launcher stopped this rank (SIGTERM), normally after another rank failed."""
+
+
+def _stopped(signum, frame):
+    raise RankStopped(f"signal {signum}: stopped by the launcher (another rank failed?)")
 
 
 def main(argv=None):
@@ -897,8 +911,17 @@ def main(argv=None):
 
     device_index = 0 if args.same_device else local
     store = None
+    if world > 1:
+        # torch.distributed.run stops every rank (SIGTERM) once one has
+        # failed: rank 0 turns that into an exception and still prints the
+        # line naming the failed rank (the launcher waits before it kills)
+        signal.signal(signal.SIGTERM, _stopped)
     try:
         store, red_dev = init_dist(args, world, device_index)
+        if args.fail_rank is not None:
+            if rank == args.fail_rank:
+                raise RuntimeError(f"injected failure on rank {rank} (--fail-rank)")
+            dist.barrier()
         rc = run_rank(args, rank, world, device_index, red_dev)
     except Exception as ex:
         rc, _ = report_failure(args, rank, world, store, ex)

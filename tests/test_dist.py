@@ -174,3 +174,27 @@ def test_bench_ranks_on_cpu_report_their_failure():
     assert line["value"] is None and sorted(line["error"]["failed_ranks"]) == [0, 1]
     assert line["config"]["dist_backend"] == "gloo"
     assert "nccl" not in r.stderr.lower()
+
+
+def test_failed_rank_named_under_torch_distributed_run():
+    """The driver's launcher: `torch.distributed.run --nproc-per-node 2
+    bench.py --gpus 2`.  Rank 1 fails right after the process group is up
+    (--fail-rank 1) while rank 0 waits in a barrier; the launcher then stops
+    the survivors.  Rank 0 still prints ONE JSON line naming rank 1 first."""
+    import json
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["HIP_VISIBLE_DEVICES"] = ""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(os.path.dirname(bench.__file__), "bench.py"), "--gpus", "2", "--fail-rank", "1",
+           "--steps", "1", "--warmup", "0", "--no-cpu-baseline"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode != 0
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout + r.stderr[-3000:]
+    line = json.loads(lines[0])
+    assert line["value"] is None and line["error"]["first"]["rank"] == 1
+    assert "injected failure on rank 1" in line["error"]["first"]["error"]
+    assert 1 in line["error"]["failed_ranks"]
