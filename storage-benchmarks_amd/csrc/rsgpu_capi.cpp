@@ -405,7 +405,11 @@ int shared_program_launch(rsgpu_ctx* ctx, const uint8_t* coef, int k, int rows, 
         j.dst_stride = rows;
         j.len = len;
         j.status = nullptr;
-        j.prio = ctx->jitw_prio;
+        // no wave priority for the shared 8-row program: (32, 8)'s encode
+        // measured 15.25 -> 17.06 ms with it, (8, 2)'s +1 % (same process
+        // ABBA x6, profiles/r06_prio/r06_prio_small_e/); the per-block 8-row
+        // decode keeps it (16, 4) -1.4 %, (64, 16) -3.2 %
+        j.prio = 0;
         KTimer kt(ctx, name, (size_t)blocks);
         RS_HIP(ctx, launch_rs_jit(j, blocks, ctx->stream));
     }
