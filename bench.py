@@ -811,7 +811,10 @@ def init_dist(args, world, device_index):
         torch.cuda.set_device(device_index)
     dist.init_process_group(args.dist_backend, init_method="env://",
                             timeout=datetime.timedelta(seconds=args.dist_timeout))
-    store = dist.distributed_c10d._get_default_store()
+    try:  # the group's own TCP store (a private accessor: failures then go unnamed)
+        store = dist.distributed_c10d._get_default_store()
+    except Exception:
+        store = None
     red = torch.device("cuda", device_index) if args.dist_backend == "nccl" else torch.device("cpu")
     return store, red
 
