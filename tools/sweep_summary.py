@@ -12,6 +12,9 @@ for f in glob.glob(os.path.join(sys.argv[1], "*.log")):
     for line in open(f):
         if line.startswith("{"):
             d = json.loads(line)
+            if d.get("value") is None:  # a failed run's line (e.g. k + e > 250)
+                print("failed:", os.path.basename(f), d.get("error", {}).get("first", {}).get("error"))
+                continue
             c = d["config"]
             ks = {k: v["avg_ms"] for k, v in d["kernels"].items() if "emit" not in k and "prepare" not in k}
             rows.append((c["symbols"], c["erased"], c["blocks_per_gpu"], d["value"], ks))
