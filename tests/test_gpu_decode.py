@@ -856,6 +856,46 @@ def test_jitw_code_prefetch(ctx, k, e, L, B):
         ctx.set_decode_kernel("auto")
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("prio", [0, 2])
+@pytest.mark.parametrize("k,e,L,B,enc_kernel", [(64, 32, 65536, 3, "compiled"), (64, 32, 32000, 9, "compiled"),
+                                                (100, 20, 6144, 3, "generated"), (32, 8, 65536, 3, "generated"),
+                                                (16, 4, 65536, 3, "compiled"), (64, 16, 32768, 2, "compiled")])
+def test_wave_priority_either_way(ctx, orc, prio, k, e, L, B, enc_kernel):
+    """The wave priority over the transposes (round 6; k_rs_bs has a second
+    instantiation without it, the generated-code kernels a runtime flag) only
+    reorders issue: with it on (2, the default) and off (0) the parity is the
+    oracle's and the recovered bytes are the originals, erased rows
+    poisoned -- compiled and generated encodes, the 16-, 10- and 8-row
+    decodes, long and short rows."""
+    import ctypes
+    h = rsgpu.testhooks()
+    f_bs, f_jw = h.rsgpu_internal_set_bs_prio, h.rsgpu_internal_set_jitw_prio
+    for f in (f_bs, f_jw):
+        f.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        assert f(ctx._h, prio) == 0
+    ctx.set_encode_kernel(enc_kernel)
+    ctx.set_decode_kernel("generated")
+    try:
+        enc = rsgpu.GpuEncoder(k, L, e, blocks=B, seed=91, ctx=ctx)
+        enc.encode_all()
+        torch.cuda.synchronize()
+        g = orc.init_tables(k, e, orc.gen_rs_matrix(k + e, k)[k:])
+        for b in (0, B - 1):
+            data = list(enc.source_rows(b))
+            ref = [np.zeros(L, np.uint8) for _ in range(e)]
+            orc.encode_data(L, k, e, g, data, ref)
+            got = enc.par.view(B, e, enc.pitch)[b, :, :L].cpu().numpy()
+            assert all((got[r] == ref[r]).all() for r in range(e)), (b, prio)
+        dec = rsgpu.GpuDecoder(k, L, e, blocks=B, seed=91, ctx=ctx)
+        assert decode_poisoned(ctx, enc, dec)
+    finally:
+        f_bs(ctx._h, 2)
+        f_jw(ctx._h, 2)
+        ctx.set_encode_kernel("auto")
+        ctx.set_decode_kernel("auto")
+
+
 def set_pipeline(ctx, n):
     import ctypes
     f = rsgpu.testhooks().rsgpu_internal_set_decode_pipeline
